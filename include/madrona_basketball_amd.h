@@ -1,0 +1,173 @@
+/*
+ * madrona_basketball_amd.h -- C ABI of the MI355X-native batched basketball
+ * simulator (the drop-in boundary for the reference's step path).
+ *
+ * Each entry point replaces one piece of the reference's Manager / nanobind
+ * surface (davidj24/madrona_basketball):
+ *
+ *   bb_create / bb_create_with_buffers
+ *       <- Manager::Manager(Config, GridState)        src/mgr.cpp:236-239
+ *          + the binding's ctor                        src/bindings.cpp:18-61
+ *   bb_destroy          <- Manager::~Manager           src/mgr.cpp:241
+ *   bb_step             <- Manager::step               src/mgr.cpp:243-246
+ *   bb_step_n           <- n x Manager::step (+ optional on-device random
+ *                          actions, the bench workload of scripts/run.py:6-19)
+ *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
+ *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
+ *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
+ *                          (exportTensor, src/mgr.cpp:74-80, 121-126)
+ *   bb_buffer_bytes     <- (new) sizes for caller-owned storage
+ *   bb_last_error       <- (new) the reference aborts via FATAL/REQ_CUDA
+ *                          (src/mgr.cpp:191,198) or printf (:289-292);
+ *                          this ABI returns status codes instead.
+ *
+ * Plain C types only.  All device pointers are HIP device pointers on the
+ * simulator's gpu_id; `stream` is a hipStream_t passed as void* (NULL = the
+ * default stream).  No function aborts; every function returns BB_OK or a
+ * negative error code and records a message for bb_last_error().
+ */
+#ifndef MADRONA_BASKETBALL_AMD_H
+#define MADRONA_BASKETBALL_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BB_ABI_VERSION 1
+
+/* status codes */
+#define BB_OK 0
+#define BB_ERR_INVALID_ARG (-1)
+#define BB_ERR_UNSUPPORTED (-2)
+#define BB_ERR_HIP (-3)
+#define BB_ERR_OOM (-4)
+
+/* madrona::ExecMode (madrona_basketball.madrona.ExecMode) */
+#define BB_EXEC_CPU 0
+#define BB_EXEC_CUDA 1   /* the HIP/gfx950 path; named as in the reference */
+
+/* dtypes reported by bb_export (madrona::py::TensorElementType subset) */
+#define BB_DTYPE_INT32 0
+#define BB_DTYPE_FLOAT32 1
+
+/* config flags */
+#define BB_FLAG_PER_WORLD_RNG 0x1u /* key each world's RNG by its global index
+                                      (reference: every world shares key
+                                      split_i(initKey(0),0,0), src/sim.cpp:89) */
+#define BB_FLAG_NO_TAG_MASK   0x2u /* drop the tag override of game.cpp:526-528 */
+#define BB_FLAG_FULL_GAME     0x4u /* isOneOnOne = 0 (constants.hpp:27 = 0) */
+
+/* Export ids: exactly src/types.hpp:10-42, then build-internal state. */
+#define BB_EXPORT_RESET 0
+#define BB_EXPORT_GAME_STATE 1
+#define BB_EXPORT_ACTION 2
+#define BB_EXPORT_ACTION_MASK 3
+#define BB_EXPORT_AGENT_POS 4
+#define BB_EXPORT_OBSERVATIONS 5
+#define BB_EXPORT_REWARD 6
+#define BB_EXPORT_DONE 7
+#define BB_EXPORT_AGENT_ENTITY_ID 8
+#define BB_EXPORT_AGENT_POSSESSION 9
+#define BB_EXPORT_ORIENTATION 10
+#define BB_EXPORT_TEAM 11
+#define BB_EXPORT_AGENT_STATS 12
+#define BB_EXPORT_BALL_POS 13
+#define BB_EXPORT_BALL_PHYSICS 14
+#define BB_EXPORT_BALL_ENTITY_ID 15
+#define BB_EXPORT_BALL_GRABBED 16
+#define BB_EXPORT_BALL_VELOCITY 17
+#define BB_EXPORT_HOOP_POS 18
+#define BB_NUM_REFERENCE_EXPORTS 19
+#define BB_INTERNAL_AGENT_VELOCITY 32
+#define BB_INTERNAL_GRAB_COOLDOWN 33
+#define BB_INTERNAL_CUR_STEP 34
+#define BB_INTERNAL_INBOUNDING 35
+#define BB_INTERNAL_ATTRIBUTES 36
+#define BB_INTERNAL_WORLD_CLOCK 37
+#define BB_INTERNAL_RNG_COUNTER 38
+#define BB_INTERNAL_FIRST 32
+#define BB_INTERNAL_LAST 38
+
+typedef struct bb_sim bb_sim;
+
+typedef struct bb_config {
+    int64_t discrete_x;          /* grid cells, cellsPerMeter = 1 (bindings.cpp:29-33) */
+    int64_t discrete_y;
+    float start_x;               /* GridState.startX/Y (ball start, spawn centre) */
+    float start_y;
+    int64_t max_episode_length;  /* accepted and ignored, as in the reference */
+    int32_t exec_mode;           /* BB_EXEC_CPU or BB_EXEC_CUDA */
+    int32_t gpu_id;              /* -1: current device */
+    int64_t num_worlds;          /* worlds owned by this simulator (this rank's shard) */
+    int64_t world_offset;        /* global index of local world 0 (sharding) */
+    uint32_t rand_seed;          /* reference hard-codes 0 (bindings.cpp:37) */
+    uint32_t flags;              /* BB_FLAG_* */
+    int32_t num_agents;          /* 2 = the reference game; 4 and 10 = extensions */
+    int32_t reserved;
+} bb_config;
+
+/* Fill *cfg with the reference defaults (scripts/env.py:20-35 constructor). */
+int bb_default_config(bb_config *cfg);
+
+/* Observation row width for num_agents (128 at 2 agents, src/types.hpp:166). */
+int32_t bb_obs_width(int32_t num_agents);
+
+/* Bytes of buffer `export_id` for cfg (caller-owned storage path). */
+int bb_buffer_bytes(const bb_config *cfg, int32_t export_id, int64_t *bytes);
+
+/* Create a simulator that allocates and owns all of its buffers. */
+int bb_create(const bb_config *cfg, bb_sim **out);
+
+/* Create a simulator over caller-owned buffers: bufs[id] for every id in
+ * [0, BB_NUM_REFERENCE_EXPORTS) and [BB_INTERNAL_FIRST, BB_INTERNAL_LAST]
+ * (nbuf = BB_INTERNAL_LAST + 1, unused slots NULL), each at least
+ * bb_buffer_bytes() long, 16-byte aligned, on the simulator's device (host
+ * memory in CPU mode).  Worlds are generated into them (src/gen.cpp:13-214). */
+int bb_create_with_buffers(const bb_config *cfg, void *const *bufs, int32_t nbuf, bb_sim **out);
+
+int bb_destroy(bb_sim *sim);
+
+/* One step of every world (the task graph of src/game.cpp:1463-1526),
+ * asynchronous on `stream` in CUDA mode, synchronous in CPU mode. */
+int bb_step(bb_sim *sim, void *stream);
+
+/* n steps.  If random_actions != 0, each step first overwrites the action
+ * tensor with the synthetic workload threefry2x32(key={action_seed, step0+s},
+ * ctr={global world, agent}) (buckets [2,8,3,2,2,2], scripts/env.py:102).
+ * If kernel_ms is non-NULL (CUDA mode), HIP events bracket every step kernel
+ * and the summed kernel time is written there after a stream sync. */
+int bb_step_n(bb_sim *sim, int32_t n, int32_t random_actions, uint32_t action_seed,
+              uint32_t step0, void *stream, float *kernel_ms);
+
+/* Only the synthetic action write (the bench's stand-in for the Python
+ * `actions[:] = ...` write of scripts/env.py:147). */
+int bb_write_random_actions(bb_sim *sim, uint32_t action_seed, uint32_t step, void *stream);
+
+int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
+                  int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,
+                  int32_t shoot, void *stream);
+
+int bb_trigger_reset(bb_sim *sim, int32_t world_idx, void *stream);
+
+/* Describe one export: data pointer (aliasing the live state), dtype and
+ * reference shape (src/mgr.cpp:317-445; ndim <= 3, dims[ndim..3] = 0). */
+int bb_export(bb_sim *sim, int32_t export_id, void **ptr, int32_t *dtype, int32_t *ndim,
+              int64_t dims[4]);
+
+/* Accessors. */
+int64_t bb_num_worlds(const bb_sim *sim);
+int32_t bb_num_agents(const bb_sim *sim);
+int32_t bb_exec_mode(const bb_sim *sim);
+
+/* Algorithmic HBM bytes moved by one step of one world (roofline). */
+int64_t bb_algorithmic_bytes_per_world(int32_t num_agents);
+
+/* Message for the last error on this thread ("" if none). */
+const char *bb_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

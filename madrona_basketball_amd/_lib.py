@@ -1,0 +1,111 @@
+"""ctypes binding of libmadrona_basketball_amd.so (include/madrona_basketball_amd.h).
+
+Loaded after `import torch`, so the library resolves libamdhip64.so.7 to the
+HIP runtime torch already loaded (one runtime per process, shared streams).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (load torch's HIP runtime first)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libmadrona_basketball_amd.so")
+
+OK = 0
+EXEC_CPU = 0
+EXEC_CUDA = 1
+DTYPE_INT32 = 0
+DTYPE_FLOAT32 = 1
+FLAG_PER_WORLD_RNG = 0x1
+FLAG_NO_TAG_MASK = 0x2
+FLAG_FULL_GAME = 0x4
+NUM_REFERENCE_EXPORTS = 19
+INTERNAL_FIRST = 32
+INTERNAL_LAST = 38
+NUM_SLOTS = INTERNAL_LAST + 1
+
+EXPORT_IDS = {
+    "reset": 0, "game_state": 1, "action": 2, "action_mask": 3, "agent_pos": 4,
+    "observations": 5, "reward": 6, "done": 7, "agent_entity_id": 8,
+    "agent_possession": 9, "orientation": 10, "team": 11, "agent_stats": 12,
+    "ball_pos": 13, "ball_physics": 14, "ball_entity_id": 15, "ball_grabbed": 16,
+    "ball_velocity": 17, "hoop_pos": 18,
+    "agent_velocity": 32, "grab_cooldown": 33, "cur_step": 34, "inbounding": 35,
+    "attributes": 36, "world_clock": 37, "rng_counter": 38,
+}
+
+# every symbol include/madrona_basketball_amd.h declares
+ABI_SYMBOLS = [
+    "bb_default_config", "bb_obs_width", "bb_buffer_bytes", "bb_create",
+    "bb_create_with_buffers", "bb_destroy", "bb_step", "bb_step_n",
+    "bb_write_random_actions", "bb_set_action", "bb_trigger_reset", "bb_export",
+    "bb_num_worlds", "bb_num_agents", "bb_exec_mode", "bb_algorithmic_bytes_per_world",
+    "bb_last_error",
+]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("discrete_x", ctypes.c_int64), ("discrete_y", ctypes.c_int64),
+        ("start_x", ctypes.c_float), ("start_y", ctypes.c_float),
+        ("max_episode_length", ctypes.c_int64),
+        ("exec_mode", ctypes.c_int32), ("gpu_id", ctypes.c_int32),
+        ("num_worlds", ctypes.c_int64), ("world_offset", ctypes.c_int64),
+        ("rand_seed", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+        ("num_agents", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+_lib = None
+
+
+class BBError(RuntimeError):
+    pass
+
+
+def load():
+    """Load (never silently replace) the native library."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -m madrona_basketball_amd.build` "
+            "(hipcc --offload-arch=gfx950). There is no Python fallback.")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
+    cfgp = ctypes.POINTER(Config)
+    sig = {
+        "bb_default_config": (ctypes.c_int, [cfgp]),
+        "bb_obs_width": (i32, [i32]),
+        "bb_buffer_bytes": (ctypes.c_int, [cfgp, i32, ctypes.POINTER(i64)]),
+        "bb_create": (ctypes.c_int, [cfgp, ctypes.POINTER(vp)]),
+        "bb_create_with_buffers": (ctypes.c_int, [cfgp, ctypes.POINTER(vp), i32, ctypes.POINTER(vp)]),
+        "bb_destroy": (ctypes.c_int, [vp]),
+        "bb_step": (ctypes.c_int, [vp, vp]),
+        "bb_step_n": (ctypes.c_int, [vp, i32, i32, u32, u32, vp, ctypes.POINTER(ctypes.c_float)]),
+        "bb_write_random_actions": (ctypes.c_int, [vp, u32, u32, vp]),
+        "bb_set_action": (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
+        "bb_trigger_reset": (ctypes.c_int, [vp, i32, vp]),
+        "bb_export": (ctypes.c_int, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(i32),
+                                     ctypes.POINTER(i32), ctypes.POINTER(i64)]),
+        "bb_num_worlds": (i64, [vp]),
+        "bb_num_agents": (i32, [vp]),
+        "bb_exec_mode": (i32, [vp]),
+        "bb_algorithmic_bytes_per_world": (i64, [i32]),
+        "bb_last_error": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != OK:
+        msg = load().bb_last_error().decode(errors="replace")
+        raise BBError(f"{what} failed ({rc}): {msg}")

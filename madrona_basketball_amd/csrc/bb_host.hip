@@ -1,0 +1,555 @@
+// bb_host.hip -- C ABI (include/madrona_basketball_amd.h) and the host executor.
+//
+// The ABI replaces the reference's Manager + nanobind class
+// (src/mgr.cpp:236-445, src/bindings.cpp:17-101).  Buffers are either owned
+// (bb_create: hipMalloc / aligned host memory) or borrowed from the caller
+// (bb_create_with_buffers: the Python layer hands in torch allocations so
+// that `to_torch()` views are native torch tensors).  In CUDA mode every
+// operation is enqueued on the caller's stream; nothing here synchronises
+// except creation and the optional kernel timing of bb_step_n.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/madrona_basketball_amd.h"
+#include "bb_launch.h"
+#include "bb_sim.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    return fail(BB_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+constexpr int NUM_SLOTS = BB_INTERNAL_LAST + 1;
+
+bool slot_used(int id)
+{
+    return (id >= 0 && id < BB_NUM_REFERENCE_EXPORTS) || (id >= BB_INTERNAL_FIRST && id <= BB_INTERNAL_LAST);
+}
+
+// Reference tensor shapes (src/mgr.cpp:317-445) + internal columns.
+bool export_info(int id, int n, int64_t W, int32_t *dtype, int32_t *ndim, int64_t dims[4], int64_t *words_per_world)
+{
+    const int64_t ow = bb::obs_width(n);
+    int32_t dt = BB_DTYPE_INT32, nd = 3;
+    int64_t d1 = n, d2 = 0;
+    switch (id) {
+    case BB_EXPORT_RESET: d2 = 1; break;
+    case BB_EXPORT_GAME_STATE: dt = BB_DTYPE_FLOAT32; nd = 2; d1 = 14; break;
+    case BB_EXPORT_ACTION: d2 = 6; break;
+    case BB_EXPORT_ACTION_MASK: d2 = 4; break;
+    case BB_EXPORT_AGENT_POS: dt = BB_DTYPE_FLOAT32; d2 = 3; break;
+    case BB_EXPORT_OBSERVATIONS: dt = BB_DTYPE_FLOAT32; d2 = ow; break;
+    case BB_EXPORT_REWARD: dt = BB_DTYPE_FLOAT32; nd = 2; break;
+    case BB_EXPORT_DONE: dt = BB_DTYPE_FLOAT32; nd = 2; break;
+    case BB_EXPORT_AGENT_ENTITY_ID: nd = 2; break;
+    case BB_EXPORT_AGENT_POSSESSION: d2 = 3; break;
+    case BB_EXPORT_ORIENTATION: dt = BB_DTYPE_FLOAT32; d2 = 4; break;
+    case BB_EXPORT_TEAM: d2 = 5; break;
+    case BB_EXPORT_AGENT_STATS: d2 = 2; break;
+    case BB_EXPORT_BALL_POS: dt = BB_DTYPE_FLOAT32; d1 = 1; d2 = 3; break;
+    case BB_EXPORT_BALL_PHYSICS: d1 = 1; d2 = 7; break;
+    case BB_EXPORT_BALL_ENTITY_ID: nd = 2; d1 = 1; break;
+    case BB_EXPORT_BALL_GRABBED: d1 = 1; d2 = 2; break;
+    case BB_EXPORT_BALL_VELOCITY: dt = BB_DTYPE_FLOAT32; d1 = 1; d2 = 3; break;
+    case BB_EXPORT_HOOP_POS: dt = BB_DTYPE_FLOAT32; d1 = 2; d2 = 3; break;
+    case BB_INTERNAL_AGENT_VELOCITY: dt = BB_DTYPE_FLOAT32; d2 = 3; break;
+    case BB_INTERNAL_GRAB_COOLDOWN: dt = BB_DTYPE_FLOAT32; nd = 2; break;
+    case BB_INTERNAL_CUR_STEP: nd = 2; break;
+    case BB_INTERNAL_INBOUNDING: d2 = 2; break;
+    case BB_INTERNAL_ATTRIBUTES: dt = BB_DTYPE_FLOAT32; d2 = 10; break;
+    case BB_INTERNAL_WORLD_CLOCK: nd = 1; d1 = 0; break;
+    case BB_INTERNAL_RNG_COUNTER: nd = 1; d1 = 0; break;
+    default: return false;
+    }
+    if (dtype) *dtype = dt;
+    if (ndim) *ndim = nd;
+    if (dims) {
+        dims[0] = W; dims[1] = nd >= 2 ? d1 : 0; dims[2] = nd >= 3 ? d2 : 0; dims[3] = 0;
+    }
+    if (words_per_world) *words_per_world = (nd == 1) ? 1 : (nd == 2 ? d1 : d1 * d2);
+    return true;
+}
+
+bool valid_agents(int n) { return n == 2 || n == 4 || n == 6 || n == 8 || n == 10; }
+
+int validate(const bb_config *cfg)
+{
+    if (!cfg) return fail(BB_ERR_INVALID_ARG, "config is NULL");
+    if (cfg->num_worlds < 1) return fail(BB_ERR_INVALID_ARG, "num_worlds must be >= 1");
+    if (cfg->discrete_x < 1 || cfg->discrete_y < 1) return fail(BB_ERR_INVALID_ARG, "discrete_x/discrete_y must be >= 1");
+    if (!valid_agents(cfg->num_agents))
+        return fail(BB_ERR_UNSUPPORTED, "num_agents must be one of 2, 4, 6, 8, 10 (reference: 2)");
+    if (cfg->exec_mode != BB_EXEC_CPU && cfg->exec_mode != BB_EXEC_CUDA)
+        return fail(BB_ERR_INVALID_ARG, "exec_mode must be BB_EXEC_CPU or BB_EXEC_CUDA");
+    if (cfg->flags & ~(BB_FLAG_PER_WORLD_RNG | BB_FLAG_NO_TAG_MASK | BB_FLAG_FULL_GAME))
+        return fail(BB_ERR_INVALID_ARG, "unknown flag bits");
+    return BB_OK;
+}
+
+int host_threads_for(int64_t worlds)
+{
+    const char *env = std::getenv("BB_CPU_THREADS");
+    int t = env ? std::atoi(env) : (int)std::thread::hardware_concurrency();
+    if (t < 1) t = 1;
+    const int64_t max_useful = (worlds + 255) / 256;
+    if (t > max_useful) t = (int)max_useful;
+    return t < 1 ? 1 : t;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool active = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (dev < 0) return;
+        if (hipGetDevice(&prev) == hipSuccess && prev != dev) {
+            if (hipSetDevice(dev) == hipSuccess) active = true;
+        }
+    }
+    ~DeviceGuard()
+    {
+        if (active) (void)hipSetDevice(prev);
+    }
+};
+
+}  // namespace
+
+struct bb_sim {
+    bb_config cfg;
+    int n = 2;
+    int device = -1;
+    bool owns = false;
+    void *slot[NUM_SLOTS] = {};
+    bb::Params p;
+};
+
+namespace {
+
+void bind_params(bb_sim *s)
+{
+    bb::Params &p = s->p;
+    std::memset(&p, 0, sizeof(p));
+    bb::Columns &c = p.c;
+    void **b = s->slot;
+    c.reset = (int32_t *)b[BB_EXPORT_RESET];
+    c.game_state = (uint32_t *)b[BB_EXPORT_GAME_STATE];
+    c.action = (int32_t *)b[BB_EXPORT_ACTION];
+    c.action_mask = (int32_t *)b[BB_EXPORT_ACTION_MASK];
+    c.agent_pos = (float *)b[BB_EXPORT_AGENT_POS];
+    c.obs = (float *)b[BB_EXPORT_OBSERVATIONS];
+    c.reward = (float *)b[BB_EXPORT_REWARD];
+    c.done = (float *)b[BB_EXPORT_DONE];
+    c.agent_id = (int32_t *)b[BB_EXPORT_AGENT_ENTITY_ID];
+    c.possession = (int32_t *)b[BB_EXPORT_AGENT_POSSESSION];
+    c.orientation = (float *)b[BB_EXPORT_ORIENTATION];
+    c.team = (uint32_t *)b[BB_EXPORT_TEAM];
+    c.stats = (float *)b[BB_EXPORT_AGENT_STATS];
+    c.ball_pos = (float *)b[BB_EXPORT_BALL_POS];
+    c.ball_physics = (int32_t *)b[BB_EXPORT_BALL_PHYSICS];
+    c.ball_id = (int32_t *)b[BB_EXPORT_BALL_ENTITY_ID];
+    c.ball_grabbed = (int32_t *)b[BB_EXPORT_BALL_GRABBED];
+    c.ball_vel = (float *)b[BB_EXPORT_BALL_VELOCITY];
+    c.hoop_pos = (float *)b[BB_EXPORT_HOOP_POS];
+    c.agent_vel = (float *)b[BB_INTERNAL_AGENT_VELOCITY];
+    c.cooldown = (float *)b[BB_INTERNAL_GRAB_COOLDOWN];
+    c.cur_step = (uint32_t *)b[BB_INTERNAL_CUR_STEP];
+    c.inbounding = (int32_t *)b[BB_INTERNAL_INBOUNDING];
+    c.attributes = (float *)b[BB_INTERNAL_ATTRIBUTES];
+    c.world_clock = (int32_t *)b[BB_INTERNAL_WORLD_CLOCK];
+    c.rng_counter = (uint32_t *)b[BB_INTERNAL_RNG_COUNTER];
+    const bb_config &cfg = s->cfg;
+    p.num_worlds = cfg.num_worlds;
+    p.world_offset = cfg.world_offset;
+    // bindings.cpp:28-33: cellsPerMeter = 1, width/height = discrete cells
+    p.width = (float)cfg.discrete_x / (float)1;
+    p.height = (float)cfg.discrete_y / (float)1;
+    p.start_x = cfg.start_x;
+    p.start_y = cfg.start_y;
+    // hoop positions (src/gen.cpp:96-141)
+    const float csx = (p.width - bb::COURT_L) / 2.0f;
+    const float ccy = p.height / 2.0f;
+    p.hoop0[0] = csx + bb::HOOP_FROM_BASE; p.hoop0[1] = ccy; p.hoop0[2] = 0.f;
+    p.hoop1[0] = csx + bb::COURT_L - bb::HOOP_FROM_BASE; p.hoop1[1] = ccy; p.hoop1[2] = 0.f;
+    p.seed = cfg.rand_seed;
+    p.flags = cfg.flags;
+}
+
+int64_t slot_bytes(const bb_config *cfg, int id)
+{
+    int64_t wpw = 0;
+    if (!export_info(id, cfg->num_agents, cfg->num_worlds, nullptr, nullptr, nullptr, &wpw)) return -1;
+    return wpw * 4 * cfg->num_worlds;
+}
+
+int init_worlds(bb_sim *s)
+{
+    if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+        DeviceGuard g(s->device);
+        for (int id = 0; id < NUM_SLOTS; id++) {
+            if (!slot_used(id)) continue;
+            hipError_t e = hipMemsetAsync(s->slot[id], 0, (size_t)slot_bytes(&s->cfg, id), nullptr);
+            if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+        }
+        hipError_t e = bb::launch_init(s->n, s->p, nullptr);
+        if (e != hipSuccess) return hip_fail(e, "launch init kernel");
+        e = hipDeviceSynchronize();
+        if (e != hipSuccess) return hip_fail(e, "world generation");
+        return BB_OK;
+    }
+    for (int id = 0; id < NUM_SLOTS; id++)
+        if (slot_used(id)) std::memset(s->slot[id], 0, (size_t)slot_bytes(&s->cfg, id));
+    return bb::host_init(s->n, s->p);
+}
+
+int create_common(const bb_config *cfg, void *const *bufs, int32_t nbuf, bb_sim **out)
+{
+    if (!out) return fail(BB_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    int rc = validate(cfg);
+    if (rc != BB_OK) return rc;
+    bb_sim *s = new bb_sim();
+    s->cfg = *cfg;
+    s->n = cfg->num_agents;
+    s->owns = bufs == nullptr;
+    if (cfg->exec_mode == BB_EXEC_CUDA) {
+        int count = 0;
+        hipError_t e = hipGetDeviceCount(&count);
+        if (e != hipSuccess || count == 0) {
+            delete s;
+            return fail(BB_ERR_HIP, "ExecMode.CUDA requested but no HIP device is available");
+        }
+        int dev = cfg->gpu_id;
+        if (dev < 0) {
+            if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+        }
+        if (dev >= count) {
+            delete s;
+            return fail(BB_ERR_INVALID_ARG, "gpu_id out of range");
+        }
+        s->device = dev;
+    }
+    for (int id = 0; id < NUM_SLOTS; id++) {
+        if (!slot_used(id)) continue;
+        const int64_t bytes = slot_bytes(cfg, id);
+        if (bufs) {
+            if (id >= nbuf || !bufs[id]) {
+                bb_destroy(s);
+                return fail(BB_ERR_INVALID_ARG, "missing caller buffer for export id " + std::to_string(id));
+            }
+            if (((uintptr_t)bufs[id]) & 15u) {
+                bb_destroy(s);
+                return fail(BB_ERR_INVALID_ARG, "caller buffer for export id " + std::to_string(id) + " is not 16-byte aligned");
+            }
+            s->slot[id] = bufs[id];
+        } else if (cfg->exec_mode == BB_EXEC_CUDA) {
+            DeviceGuard g(s->device);
+            void *ptr = nullptr;
+            hipError_t e = hipMalloc(&ptr, (size_t)bytes);
+            if (e != hipSuccess) {
+                bb_destroy(s);
+                return fail(BB_ERR_OOM, std::string("hipMalloc failed: ") + hipGetErrorString(e));
+            }
+            s->slot[id] = ptr;
+        } else {
+            void *ptr = std::aligned_alloc(64, (size_t)((bytes + 63) & ~int64_t(63)));
+            if (!ptr) {
+                bb_destroy(s);
+                return fail(BB_ERR_OOM, "host allocation failed");
+            }
+            s->slot[id] = ptr;
+        }
+    }
+    bind_params(s);
+    rc = init_worlds(s);
+    if (rc != BB_OK) {
+        bb_destroy(s);
+        return rc;
+    }
+    *out = s;
+    return BB_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host executor
+namespace bb {
+
+template <int N>
+static void host_range(const Params &p, int64_t lo, int64_t hi)
+{
+    for (int64_t w = lo; w < hi; w++) step_one_world<N>(p, w);
+}
+
+template <int N>
+static int host_step_n(const Params &p, int threads)
+{
+    const int64_t W = p.num_worlds;
+    if (threads <= 1) {
+        host_range<N>(p, 0, W);
+        return BB_OK;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve((size_t)threads);
+    for (int t = 0; t < threads; t++) {
+        const int64_t lo = W * t / threads, hi = W * (t + 1) / threads;
+        pool.emplace_back([&p, lo, hi] { host_range<N>(p, lo, hi); });
+    }
+    for (auto &th : pool) th.join();
+    return BB_OK;
+}
+
+template <int N>
+static int host_init_n(const Params &p)
+{
+    for (int64_t w = 0; w < p.num_worlds; w++) init_world<N>(p, w);
+    return BB_OK;
+}
+
+int host_step(int n, const Params &p, int threads)
+{
+    switch (n) {
+    case 2: return host_step_n<2>(p, threads);
+    case 4: return host_step_n<4>(p, threads);
+    case 6: return host_step_n<6>(p, threads);
+    case 8: return host_step_n<8>(p, threads);
+    case 10: return host_step_n<10>(p, threads);
+    default: return BB_ERR_UNSUPPORTED;
+    }
+}
+
+int host_init(int n, const Params &p)
+{
+    switch (n) {
+    case 2: return host_init_n<2>(p);
+    case 4: return host_init_n<4>(p);
+    case 6: return host_init_n<6>(p);
+    case 8: return host_init_n<8>(p);
+    case 10: return host_init_n<10>(p);
+    default: return BB_ERR_UNSUPPORTED;
+    }
+}
+
+int host_random_actions(int n, const Params &p, uint32_t seed, uint32_t step)
+{
+    for (int64_t w = 0; w < p.num_worlds; w++)
+        for (int a = 0; a < n; a++)
+            random_action(seed, step, (uint32_t)(p.world_offset + w), (uint32_t)a, p.c.action + (w * n + a) * 6);
+    return BB_OK;
+}
+
+}  // namespace bb
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+int bb_default_config(bb_config *cfg)
+{
+    if (!cfg) return fail(BB_ERR_INVALID_ARG, "config is NULL");
+    std::memset(cfg, 0, sizeof(*cfg));
+    // scripts/env.py:20-35 with src/constants.py WORLD_WIDTH_M/HEIGHT_M
+    cfg->discrete_x = 32;
+    cfg->discrete_y = 17;
+    cfg->start_x = (float)(31.515 / 2.0);
+    cfg->start_y = (float)(16.764000000000003 / 2.0);
+    cfg->max_episode_length = 39600;
+    cfg->exec_mode = BB_EXEC_CPU;
+    cfg->gpu_id = 0;
+    cfg->num_worlds = 1;
+    cfg->world_offset = 0;
+    cfg->rand_seed = 0;
+    cfg->flags = 0;
+    cfg->num_agents = 2;
+    return BB_OK;
+}
+
+int32_t bb_obs_width(int32_t num_agents) { return bb::obs_width(num_agents); }
+
+int bb_buffer_bytes(const bb_config *cfg, int32_t export_id, int64_t *bytes)
+{
+    int rc = validate(cfg);
+    if (rc != BB_OK) return rc;
+    if (!bytes) return fail(BB_ERR_INVALID_ARG, "bytes is NULL");
+    const int64_t b = slot_bytes(cfg, export_id);
+    if (b < 0) return fail(BB_ERR_INVALID_ARG, "unknown export id " + std::to_string(export_id));
+    *bytes = b;
+    return BB_OK;
+}
+
+int bb_create(const bb_config *cfg, bb_sim **out) { return create_common(cfg, nullptr, 0, out); }
+
+int bb_create_with_buffers(const bb_config *cfg, void *const *bufs, int32_t nbuf, bb_sim **out)
+{
+    if (!bufs) return fail(BB_ERR_INVALID_ARG, "bufs is NULL");
+    return create_common(cfg, bufs, nbuf, out);
+}
+
+int bb_destroy(bb_sim *s)
+{
+    if (!s) return BB_OK;
+    if (s->owns) {
+        for (int id = 0; id < NUM_SLOTS; id++) {
+            if (!s->slot[id]) continue;
+            if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+                DeviceGuard g(s->device);
+                (void)hipFree(s->slot[id]);
+            } else {
+                std::free(s->slot[id]);
+            }
+        }
+    }
+    delete s;
+    return BB_OK;
+}
+
+int bb_step(bb_sim *s, void *stream)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+        DeviceGuard g(s->device);
+        hipError_t e = bb::launch_step(s->n, s->p, (hipStream_t)stream);
+        if (e != hipSuccess) return hip_fail(e, "launch step kernel");
+        return BB_OK;
+    }
+    return bb::host_step(s->n, s->p, host_threads_for(s->cfg.num_worlds));
+}
+
+int bb_write_random_actions(bb_sim *s, uint32_t action_seed, uint32_t step, void *stream)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+        DeviceGuard g(s->device);
+        hipError_t e = bb::launch_random_actions(s->n, s->p, action_seed, step, (hipStream_t)stream);
+        if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
+        return BB_OK;
+    }
+    return bb::host_random_actions(s->n, s->p, action_seed, step);
+}
+
+int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed, uint32_t step0,
+              void *stream, float *kernel_ms)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    if (n < 0) return fail(BB_ERR_INVALID_ARG, "n must be >= 0");
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) {
+        for (int32_t k = 0; k < n; k++) {
+            if (random_actions) bb::host_random_actions(s->n, s->p, action_seed, step0 + (uint32_t)k);
+            int rc = bb::host_step(s->n, s->p, host_threads_for(s->cfg.num_worlds));
+            if (rc != BB_OK) return rc;
+        }
+        if (kernel_ms) *kernel_ms = 0.f;
+        return BB_OK;
+    }
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<hipEvent_t> ev;
+    if (kernel_ms && n > 0) {
+        ev.resize((size_t)2 * n);
+        for (auto &e : ev) {
+            hipError_t he = hipEventCreate(&e);
+            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
+        }
+    }
+    for (int32_t k = 0; k < n; k++) {
+        if (random_actions) {
+            hipError_t e = bb::launch_random_actions(s->n, s->p, action_seed, step0 + (uint32_t)k, st);
+            if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
+        }
+        if (!ev.empty()) (void)hipEventRecord(ev[2 * k], st);
+        hipError_t e = bb::launch_step(s->n, s->p, st);
+        if (e != hipSuccess) return hip_fail(e, "launch step kernel");
+        if (!ev.empty()) (void)hipEventRecord(ev[2 * k + 1], st);
+    }
+    if (!ev.empty()) {
+        hipError_t e = hipEventSynchronize(ev.back());
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        double total = 0.0;
+        for (int32_t k = 0; k < n; k++) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+            total += ms;
+        }
+        for (auto &x : ev) (void)hipEventDestroy(x);
+        *kernel_ms = (float)total;
+    }
+    return BB_OK;
+}
+
+int bb_set_action(bb_sim *s, int32_t world_idx, int32_t agent_idx, int32_t move_speed, int32_t move_angle,
+                  int32_t rotate, int32_t grab, int32_t pass, int32_t shoot, void *stream)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    if (world_idx < 0 || world_idx >= s->cfg.num_worlds || agent_idx < 0 || agent_idx >= s->n) {
+        char msg[160];
+        std::snprintf(msg, sizeof(msg), "Invalid indices! world=%d (max=%lld), agent=%d (max=%d)", world_idx,
+                      (long long)s->cfg.num_worlds - 1, agent_idx, s->n - 1);
+        return fail(BB_ERR_INVALID_ARG, msg);
+    }
+    const int32_t vals[6] = {move_speed, move_angle, rotate, grab, pass, shoot};
+    int32_t *dst = s->p.c.action + ((int64_t)world_idx * s->n + agent_idx) * 6;
+    if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+        DeviceGuard g(s->device);
+        hipError_t e = bb::launch_poke(dst, 6, vals, (hipStream_t)stream);
+        if (e != hipSuccess) return hip_fail(e, "set_action");
+        return BB_OK;
+    }
+    std::memcpy(dst, vals, sizeof(vals));
+    return BB_OK;
+}
+
+int bb_trigger_reset(bb_sim *s, int32_t world_idx, void *stream)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    // src/mgr.cpp:303: an out-of-range world is silently ignored
+    if (world_idx < 0 || world_idx >= s->cfg.num_worlds) return BB_OK;
+    int32_t *dst = s->p.c.reset + (int64_t)world_idx * s->n;
+    int32_t vals[8];
+    for (int k = 0; k < 8; k++) vals[k] = 1;
+    if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+        DeviceGuard g(s->device);
+        hipError_t e = bb::launch_poke(dst, s->n, vals, (hipStream_t)stream);
+        if (e != hipSuccess) return hip_fail(e, "trigger_reset");
+        return BB_OK;
+    }
+    for (int k = 0; k < s->n; k++) dst[k] = 1;
+    return BB_OK;
+}
+
+int bb_export(bb_sim *s, int32_t export_id, void **ptr, int32_t *dtype, int32_t *ndim, int64_t dims[4])
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
+    if (!slot_used(export_id)) return fail(BB_ERR_INVALID_ARG, "unknown export id " + std::to_string(export_id));
+    if (!export_info(export_id, s->n, s->cfg.num_worlds, dtype, ndim, dims, nullptr))
+        return fail(BB_ERR_INVALID_ARG, "unknown export id");
+    if (ptr) *ptr = s->slot[export_id];
+    return BB_OK;
+}
+
+int64_t bb_num_worlds(const bb_sim *s) { return s ? s->cfg.num_worlds : 0; }
+int32_t bb_num_agents(const bb_sim *s) { return s ? s->n : 0; }
+int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
+
+int64_t bb_algorithmic_bytes_per_world(int32_t n)
+{
+    // B(N) = N (268 + 4 obs_used(N)) + 152
+    return (int64_t)n * (268 + 4 * (int64_t)bb::obs_used(n)) + 152;
+}
+
+const char *bb_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,1308 @@
+// bb_sim.h -- the basketball world step, compiled for gfx950 and for the host.
+//
+// One world = one register-resident `World<N>`; `step_world` runs the 19
+// systems of the reference task graph (src/game.cpp:1463-1526) in graph order,
+// agents in creation order, exactly as the Madrona CPU TaskGraphExecutor
+// sequences them.  The gfx950 kernel (bb_step.hip) maps one world to one lane:
+// load -> step_world -> store, so every cross-entity `ctx.get<>` of the
+// reference becomes a register access.
+//
+// HBM layout = the reference's export layout (world-major component columns,
+// src/mgr.cpp:317-445) for every exported component, plus world-major columns
+// for the build-internal state (velocity, cooldown, ...).  See DESIGN.md.
+#pragma once
+#include <stdint.h>
+#include "bb_math.h"
+#include "bb_rng.h"
+
+namespace bb {
+
+// ------------------------------------------------------------------ constants
+// src/constants.hpp, evaluated in float exactly like the C++ constexprs.
+constexpr float PI = 3.14159265358979323846f;                 // madrona::math::pi
+constexpr float TS = 1.0f / 62.0f;                            // :12
+constexpr float TIME_PER_PERIOD = 10.f;                       // :13
+constexpr float PPM = 110.f;                                  // :17
+constexpr float HOOP_ZONE = 0.1f;                             // :24
+constexpr float AGENT_SIZE = 0.2f;                            // :39
+constexpr float SHOULDER = 0.4290;                            // :40
+constexpr float DEPTH = .1;                                   // :41
+constexpr float GUARD = .2f;                                  // :45
+constexpr float START_STD = 5.f;                              // :46
+constexpr float DEFAULT_SPEED = 3.f;                          // :47
+constexpr float DEF_SLOW = 0.2f;                              // :48
+constexpr float DEF_REACT = 10.f;                             // :49
+constexpr float SPAWN_R = 8.f;                                // :50
+constexpr float ANGLE_STEP = PI / 4.0f;                       // :53
+constexpr float BALL_SLOW = 0.9f;                             // :55
+constexpr float DIST_DEV = .008f, DEF_DEV = .002f, VEL_DEV = .001f;  // :59-61
+constexpr float COURT_L = 28.65f, COURT_W = 15.24f;          // :67-68
+constexpr float WORLD_W = COURT_L * 1.1f;                     // :72
+constexpr float WORLD_H = COURT_W * 1.1f;                     // :73
+constexpr float CMINX = (WORLD_W - COURT_L) / 2.0f;           // :76
+constexpr float CMAXX = CMINX + COURT_L;                      // :77
+constexpr float CMINY = (WORLD_H - COURT_W) / 2.0f;           // :78
+constexpr float CMAXY = CMINY + COURT_W;                      // :79
+constexpr float HOOP_FROM_BASE = 1.575f;                      // :84
+constexpr float ARC = 7.24f, CORNER_SIDE = 0.91f, CORNER_LEN = 4.27f;  // :91-93
+constexpr float CORNER_LO_Y = CMINY + CORNER_SIDE;            // helper.cpp:55
+constexpr float CORNER_HI_Y = CMINY + COURT_W - CORNER_SIDE;  // helper.cpp:56
+constexpr float CORNER_LEFT_X = CMINX + CORNER_LEN;           // helper.cpp:63
+constexpr float CORNER_RIGHT_X = CMINX + COURT_L - CORNER_LEN;  // helper.cpp:67
+constexpr float HALF_WORLD_W = WORLD_W / 2.0f;                // helper.cpp:60
+constexpr float INBOUND_DY = PPM / 60;                        // game.cpp:918
+constexpr float HALF_SHOULDER = SHOULDER / 2.0f;              // game.cpp:561
+constexpr float HALF_DEPTH = DEPTH / 2.0f;                    // game.cpp:562
+constexpr float TURN_POS = (PI / 180.f) * 6;                  // game.cpp:423
+constexpr float TURN_NEG = (PI / 180.f) * -6;
+constexpr float PI_OVER_8 = PI / 8.f;                         // game.cpp:747
+constexpr int32_t PH = 2147483647;                            // ENTITY_ID_PLACEHOLDER
+// Build-defined entity ids (creation order of src/gen.cpp:101-206).
+constexpr int32_t HOOP0_ID = 0, HOOP1_ID = 1, BALL_ID = 2, AGENT0_ID = 3;
+
+constexpr uint32_t FLAG_PER_WORLD_RNG = 0x1u, FLAG_NO_TAG_MASK = 0x2u, FLAG_FULL_GAME = 0x4u;
+
+BB_HD constexpr int obs_used(int n) { return 61 + 38 * (n - 1) + 2 * n; }
+BB_HD constexpr int obs_width(int n)
+{
+    return ((obs_used(n) + 3) & ~3) < 128 ? 128 : ((obs_used(n) + 3) & ~3);
+}
+
+// ------------------------------------------------------------------ vec math
+// madrona::math::Vector3 / Quat operations, in the reference's operand order.
+struct F3 { float x, y, z; };
+struct Q4 { float w, x, y, z; };
+BB_HD F3 f3(float x, float y, float z) { F3 r; r.x = x; r.y = y; r.z = z; return r; }
+BB_HD F3 operator+(F3 a, F3 b) { return f3(a.x + b.x, a.y + b.y, a.z + b.z); }
+BB_HD F3 operator-(F3 a, F3 b) { return f3(a.x - b.x, a.y - b.y, a.z - b.z); }
+BB_HD F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }
+BB_HD F3 operator*(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
+BB_HD float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+BB_HD float len2(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+BB_HD float len(F3 a) { return bbm::sqrtf_(len2(a)); }
+// Vector3::normalize: unpinned Madrona detail, fixed as v * (1 / |v|).
+BB_HD F3 norm(F3 a) { return a * (1.0f / bbm::sqrtf_(len2(a))); }
+BB_HD F3 cross(F3 a, F3 b)
+{
+    return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+BB_HD float clampf(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+BB_HD float minf(float a, float b) { return b < a ? b : a; }
+BB_HD float maxf(float a, float b) { return b > a ? b : a; }
+BB_HD Q4 quat_axis_z(float angle, float axis_z)  // Quat::angleAxis(angle, {0,0,axis_z})
+{
+    float s, c;
+    bbm::sincosf_(0.5f * angle, &s, &c);
+    Q4 q; q.w = c; q.x = s * 0.f; q.y = s * 0.f; q.z = s * axis_z; return q;
+}
+BB_HD Q4 quat_axis(float angle, F3 n)
+{
+    float s, c;
+    bbm::sincosf_(0.5f * angle, &s, &c);
+    Q4 q; q.w = c; q.x = s * n.x; q.y = s * n.y; q.z = s * n.z; return q;
+}
+BB_HD Q4 qmul(Q4 a, Q4 b)
+{
+    Q4 r;
+    r.w = a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z;
+    r.x = a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y;
+    r.y = a.w * b.y - a.x * b.z + a.y * b.w + a.z * b.x;
+    r.z = a.w * b.z + a.x * b.y - a.y * b.x + a.z * b.w;
+    return r;
+}
+// Quat::rotateVec (pinned by scripts/viewer.py:59-65)
+BB_HD F3 rotate(Q4 q, F3 v)
+{
+    const F3 p = f3(q.x, q.y, q.z);
+    const F3 pv = cross(p, v);
+    const F3 ppv = cross(p, pv);
+    return v + ((pv * q.w) + ppv) * 2.f;
+}
+// rotate(q, (0,1,0)), the agent's forward vector
+BB_HD F3 forward(Q4 q) { return rotate(q, f3(0.f, 1.f, 0.f)); }
+
+// findRotationBetweenVectors(AGENT_BASE_FORWARD, t)  (src/helper.cpp:14-42)
+BB_HD Q4 rotation_from_forward(F3 t)
+{
+    const F3 a = norm(f3(0.f, 1.f, 0.f));
+    t = norm(t);
+    const float d = dot(a, t);
+    if (d > 0.999999f) { Q4 id; id.w = 1.f; id.x = 0.f; id.y = 0.f; id.z = 0.f; return id; }
+    if (d < -0.999999f) return quat_axis_z(PI, 1.f);
+    const F3 ax = norm(cross(a, t));
+    return quat_axis(bbm::acosf_(d), ax);
+}
+
+// getShotPointValue (src/helper.cpp:50-81)
+BB_HD int32_t shot_point_value(F3 p, F3 hz)
+{
+    const float d = len(p - hz);
+    if (p.y < CORNER_LO_Y || p.y > CORNER_HI_Y) {
+        if (hz.x < HALF_WORLD_W) { if (p.x <= CORNER_LEFT_X) return 3; }
+        else { if (p.x >= CORNER_RIGHT_X) return 3; }
+    }
+    return d >= ARC ? 3 : 2;
+}
+
+// ------------------------------------------------------------------ layout
+// Column pointers.  Exported columns keep the reference byte layouts;
+// *_u views reinterpret mixed int/float structs (GameState, Team, Stats).
+struct Columns {
+    int32_t *reset;        // [W][N]            Reset
+    uint32_t *game_state;  // [W][14]           GameState (mixed i32/f32, exported as f32)
+    int32_t *action;       // [W][N][6]         Action
+    int32_t *action_mask;  // [W][N][4]         ActionMask
+    float *agent_pos;      // [W][N][3]         Position
+    float *obs;            // [W][N][OBSW]      Observations
+    float *reward;         // [W][N]            Reward
+    float *done;           // [W][N]            Done
+    int32_t *agent_id;     // [W][N]            Entity (build ids)
+    int32_t *possession;   // [W][N][3]         InPossession
+    float *orientation;    // [W][N][4]         Orientation (w,x,y,z)
+    uint32_t *team;        // [W][N][5]         Team {i32, f32 x3, i32}
+    float *stats;          // [W][N][2]         Stats (exported as i32)
+    float *ball_pos;       // [W][1][3]
+    int32_t *ball_physics; // [W][1][7]
+    int32_t *ball_id;      // [W][1]
+    int32_t *ball_grabbed; // [W][1][2]
+    float *ball_vel;       // [W][1][3]
+    float *hoop_pos;       // [W][2][3]
+    // build-internal state
+    float *agent_vel;      // [W][N][3]
+    float *cooldown;       // [W][N]
+    uint32_t *cur_step;    // [W][N]
+    int32_t *inbounding;   // [W][N][2]
+    float *attributes;     // [W][N][10]  maxSpeed quick shoot ft react tgt.xyz shotPct pad
+    int32_t *world_clock;  // [W]
+    uint32_t *rng_counter; // [W]
+};
+
+struct Params {
+    Columns c;
+    int64_t num_worlds;
+    int64_t world_offset;
+    float width, height, start_x, start_y;
+    float hoop0[3], hoop1[3];
+    uint32_t seed, flags;
+};
+
+BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+BB_HD float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// Vector-width chunk load/store of NW consecutive 32-bit words (16-B, 8-B or
+// 4-B wide accesses depending on the chunk's alignment).
+template <int NW>
+BB_HD void load_words(const void *base, int64_t w, uint32_t (&o)[NW])
+{
+    const uint32_t *p = (const uint32_t *)base + w * NW;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (NW % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW / 4; k++) {
+            const uint4 v = ((const uint4 *)p)[k];
+            o[4 * k] = v.x; o[4 * k + 1] = v.y; o[4 * k + 2] = v.z; o[4 * k + 3] = v.w;
+        }
+    } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW / 2; k++) {
+            const uint2 v = ((const uint2 *)p)[k];
+            o[2 * k] = v.x; o[2 * k + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW; k++) o[k] = p[k];
+    }
+#else
+    __builtin_memcpy(o, p, sizeof(o));
+#endif
+}
+
+template <int NW>
+BB_HD void store_words(void *base, int64_t w, const uint32_t (&o)[NW])
+{
+    uint32_t *p = (uint32_t *)base + w * NW;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (NW % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW / 4; k++)
+            ((uint4 *)p)[k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+        for (int k = 0; k < NW / 2; k++) ((uint2 *)p)[k] = make_uint2(o[2 * k], o[2 * k + 1]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW; k++) p[k] = o[k];
+    }
+#else
+    __builtin_memcpy(p, o, sizeof(o));
+#endif
+}
+
+BB_HD void store_f4(float *p, float a, float b, float c, float d)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    *(float4 *)p = make_float4(a, b, c, d);
+#else
+    p[0] = a; p[1] = b; p[2] = c; p[3] = d;
+#endif
+}
+
+// ------------------------------------------------------------------ state
+template <int N>
+struct World {
+    // GameState singleton (src/types.hpp:46-67)
+    int32_t g_inb, g_live; float g_period, g_poss; int32_t g_h0; float g_s0; int32_t g_h1;
+    float g_s1, g_clock, g_shot, g_bask, g_oob, g_inbclk; int32_t g_1v1;
+    int32_t reset_now;   // WorldClock singleton
+    uint32_t rng_ctr;    // Sim::rng draw counter
+    // agents
+    int32_t rst[N], act[N][6], msk[N][4];
+    float cd[N], px[N], py[N], pz[N], rew[N], done[N];
+    uint32_t step[N];
+    int32_t has[N], bid[N], pw[N];
+    float qw[N], qx[N], qy[N], qz[N];
+    int32_t inb[N], allow[N], team[N], dhoop[N];
+    float attr[N][10];   // maxSpeed quickness shooting ft reaction tx ty tz shotPct pad
+    float vx[N], vy[N], vz[N];
+    // ball
+    float bx, by, bz, bvx, bvy, bvz;
+    int32_t fl, lta, ltt, sba, sbt, spv, gin;  // BallPhysics
+    int32_t grab, holder;                      // Grabbed
+
+    BB_HD F3 pos(int i) const { return f3(px[i], py[i], pz[i]); }
+    BB_HD void set_pos(int i, F3 v) { px[i] = v.x; py[i] = v.y; pz[i] = v.z; }
+    BB_HD F3 vel(int i) const { return f3(vx[i], vy[i], vz[i]); }
+    BB_HD void set_vel(int i, F3 v) { vx[i] = v.x; vy[i] = v.y; vz[i] = v.z; }
+    BB_HD Q4 q(int i) const { Q4 r; r.w = qw[i]; r.x = qx[i]; r.y = qy[i]; r.z = qz[i]; return r; }
+    BB_HD void set_q(int i, Q4 v) { qw[i] = v.w; qx[i] = v.x; qy[i] = v.y; qz[i] = v.z; }
+    BB_HD F3 bpos() const { return f3(bx, by, bz); }
+    BB_HD void set_bpos(F3 v) { bx = v.x; by = v.y; bz = v.z; }
+    BB_HD F3 bvel() const { return f3(bvx, bvy, bvz); }
+    BB_HD void set_bvel(F3 v) { bvx = v.x; bvy = v.y; bvz = v.z; }
+    BB_HD F3 target(int i) const { return f3(attr[i][5], attr[i][6], attr[i][7]); }
+    BB_HD void set_target(int i, F3 v) { attr[i][5] = v.x; attr[i][6] = v.y; attr[i][7] = v.z; }
+};
+
+// Per-world execution context: world index, RNG key cache, side channel for
+// the rarely written columns (Stats, Team colour) that are not kept in
+// registers.
+struct Ctx {
+    const Params *p;
+    int64_t w;
+    uint32_t k0, k1;
+    bool key_ready;
+};
+
+template <int N>
+BB_HD float sample_uniform(World<N> &s, Ctx &c, float lo, float hi)
+{
+    if (!c.key_ready) {
+        const uint32_t idx = (c.p->flags & FLAG_PER_WORLD_RNG) ? (uint32_t)(c.p->world_offset + c.w) : 0u;
+        threefry2x32(c.p->seed, 0u, idx, 0u, &c.k0, &c.k1);
+        c.key_ready = true;
+    }
+    uint32_t r0, r1;
+    threefry2x32(c.k0, c.k1, s.rng_ctr, 0u, &r0, &r1);
+    s.rng_ctr++;
+    return lo + (hi - lo) * u01_from_bits(r0);
+}
+
+template <int N>
+BB_HD F3 hoop_pos(const Ctx &c, int h)
+{
+    const float *hp = h == 0 ? c.p->hoop0 : c.p->hoop1;
+    return f3(hp[0], hp[1], hp[2]);
+}
+
+BB_HD F3 vec_to_center(const Ctx &c, F3 p)  // findVectorToCenter, helper.cpp:44-48
+{
+    return norm(f3(c.p->start_x, c.p->start_y, 0.f) - p);
+}
+
+// ------------------------------------------------------------------ gen/reset
+template <int N>
+BB_HD Q4 start_orientation(int i)  // gen.cpp:196 / :277
+{
+    return (i % 2 == 0) ? quat_axis_z(-PI / 2.0f, 1.f) : quat_axis_z(PI / 2.0f, 1.f);
+}
+
+// setupAgentPositions (src/helper.cpp:108-160); returns the ball holder id.
+template <int N>
+BB_HD int32_t setup_agent_positions(World<N> &s, Ctx &c, F3 *ball_at)
+{
+    int32_t off_id = PH;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.g_1v1 == 1) {
+            if (i == 0) {
+                const F3 base = f3(c.p->start_x + ((float)i * 2.f), c.p->start_y, 0.f);
+                const float xd = sample_uniform(s, c, -START_STD, START_STD);
+                const float yd = sample_uniform(s, c, -START_STD, START_STD);
+                F3 p = base + f3(xd, yd, 0.f);
+                p.x = clampf(p.x, 0.f, c.p->width);
+                p.y = clampf(p.y, 0.f, c.p->height);
+                s.set_pos(i, p);
+                *ball_at = p;
+                off_id = AGENT0_ID + i;
+                s.has[i] = 1; s.bid[i] = BALL_ID; s.pw[i] = 2;
+            } else {
+                const float ang = sample_uniform(s, c, 0.f, 2.f * PI);
+                float sn, cs;
+                bbm::sincosf_(ang, &sn, &cs);
+                F3 p = *ball_at + f3(SPAWN_R * cs, SPAWN_R * sn, 0.f);
+                p.x = clampf(p.x, 0.f, c.p->width);
+                p.y = clampf(p.y, 0.f, c.p->height);
+                s.set_pos(i, p);
+                s.has[i] = 0; s.bid[i] = PH; s.pw[i] = 2;
+            }
+        } else {
+            s.set_pos(i, f3((c.p->start_x - 1.f) - (float)(-2 * (i % 2)),
+                            (c.p->start_y - 2.f) + (float)(i / 2), 0.f));
+            if (i == 0) { off_id = AGENT0_ID + i; s.has[i] = 1; s.bid[i] = BALL_ID; s.pw[i] = 2; }
+            else { s.has[i] = 0; s.bid[i] = PH; s.pw[i] = 2; }
+        }
+        s.attr[i][0] = DEFAULT_SPEED - (float)i * DEF_SLOW;
+        s.attr[i][1] = 1.f; s.attr[i][2] = 0.f; s.attr[i][3] = 0.f;
+        s.attr[i][4] = (float)i * DEF_REACT;
+        s.set_target(i, s.pos(i));
+        s.attr[i][8] = 0.f; s.attr[i][9] = 0.f;
+    }
+    return off_id;
+}
+
+// Team column write (rare: generation and resets).
+template <int N>
+BB_HD void write_team(const Ctx &c, int i, int32_t team, F3 color, int32_t dhoop)
+{
+    uint32_t *t = c.p->c.team + (c.w * N + i) * 5;
+    t[0] = (uint32_t)team; t[1] = fbits(color.x); t[2] = fbits(color.y); t[3] = fbits(color.z);
+    t[4] = (uint32_t)dhoop;
+}
+
+// generateWorld (src/gen.cpp:13-214) + Sim::Sim rng seeding (src/sim.cpp:86-96)
+template <int N>
+BB_HD void generate_world(World<N> &s, Ctx &c)
+{
+    s.g_inb = 0; s.g_live = 1; s.g_period = 1.f; s.g_poss = 0.f; s.g_h0 = HOOP0_ID; s.g_s0 = 0.f;
+    s.g_h1 = HOOP1_ID; s.g_s1 = 0.f; s.g_clock = TIME_PER_PERIOD; s.g_shot = 24.f; s.g_bask = 0.f;
+    s.g_oob = 0.f; s.g_inbclk = 0.f; s.g_1v1 = (c.p->flags & FLAG_FULL_GAME) ? 0 : 1;
+    s.reset_now = 0;
+    s.rng_ctr = 0;
+    s.bx = c.p->start_x; s.by = c.p->start_y; s.bz = 0.f;
+    s.grab = 0; s.holder = PH;
+    s.fl = 0; s.lta = PH; s.ltt = PH; s.sba = PH; s.sbt = PH; s.spv = 2; s.gin = 0;
+    s.bvx = 0.f; s.bvy = 0.f; s.bvz = 0.f;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) s.act[i][k] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.msk[i][k] = 0;
+        s.rst[i] = 0; s.inb[i] = 0; s.allow[i] = 1; s.rew[i] = 0.f; s.done[i] = 0.f; s.step[i] = 0;
+        s.set_q(i, start_orientation<N>(i));
+        s.cd[i] = 0.f;
+        s.vx[i] = 0.f; s.vy[i] = 0.f; s.vz[i] = 0.f;
+        s.team[i] = i % 2;
+        s.dhoop[i] = (i % 2 == 0) ? s.g_h0 : s.g_h1;
+        s.has[i] = 0; s.bid[i] = 0; s.pw[i] = 0;
+        s.px[i] = 0.f; s.py[i] = 0.f; s.pz[i] = 0.f;
+        write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(128.f, 0.f, 128.f),
+                      s.dhoop[i]);
+        float *st = c.p->c.stats + (c.w * N + i) * 2;
+        st[0] = 0.f; st[1] = 0.f;
+    }
+    F3 ball_at = f3(c.p->start_x, c.p->start_y, 0.f);
+    const int32_t off_id = setup_agent_positions(s, c, &ball_at);
+    if (s.g_1v1 == 1) { s.grab = 1; s.holder = off_id; }
+}
+
+// resetWorld (src/gen.cpp:216-316)
+template <int N>
+BB_HD void reset_world(World<N> &s, Ctx &c)
+{
+    if (s.g_clock <= 0.f && (float)s.g_1v1 == 0.f) {
+        if (s.g_period < 4.f || s.g_s0 == s.g_s1) {
+            s.g_period += 1.f; s.g_clock = TIME_PER_PERIOD; s.g_shot = 24.f; s.g_live = 1; s.g_inb = 0;
+        } else {
+            s.g_live = 0;
+        }
+    } else {
+        s.g_inb = 0; s.g_live = 1; s.g_period = 1.f; s.g_poss = 0.f; s.g_s0 = 0.f; s.g_s1 = 0.f;
+        s.g_clock = TIME_PER_PERIOD; s.g_shot = 24.f; s.g_bask = 0.f; s.g_oob = 0.f; s.g_inbclk = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+#pragma unroll
+        for (int k = 0; k < 6; k++) s.act[i][k] = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.msk[i][k] = 0;
+        s.rst[i] = 0; s.inb[i] = 0; s.allow[i] = 1; s.done[i] = 1.f; s.step[i] = 0;
+        s.set_q(i, start_orientation<N>(i));
+        s.cd[i] = 0.f;
+        s.vx[i] = 0.f; s.vy[i] = 0.f; s.vz[i] = 0.f;
+        s.team[i] = i % 2;
+        s.dhoop[i] = (i % 2 == 0) ? s.g_h0 : s.g_h1;
+        write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(255.f, 0.f, 100.f),
+                      s.dhoop[i]);
+        float *st = c.p->c.stats + (c.w * N + i) * 2;
+        st[0] = 0.f; st[1] = 0.f;
+    }
+    F3 ball_at = f3(c.p->start_x, c.p->start_y, 0.f);
+    const int32_t off_id = setup_agent_positions(s, c, &ball_at);
+    s.set_bpos(ball_at);
+    s.fl = 0; s.lta = PH; s.ltt = PH; s.sba = PH; s.sbt = PH; s.spv = 2; s.gin = 0;
+    s.bvx = 0.f; s.bvy = 0.f; s.bvz = 0.f;
+    if (s.g_1v1 == 1) { s.grab = 1; s.holder = off_id; }
+    else { s.grab = 0; s.holder = PH; }
+}
+
+// assignInbounder (src/game.cpp:14-53)
+template <int N>
+BB_HD void assign_inbounder(World<N> &s, F3 ball_pos, int32_t new_team, Q4 orient, bool is_oob)
+{
+    float assigned = 0.0f;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.team[i] == new_team && assigned == 0.f) {
+            assigned = 1.f;
+            s.inb[i] = 1;
+            s.set_pos(i, ball_pos);
+            s.grab = 1; s.holder = AGENT0_ID + i;
+            s.has[i] = 1; s.bid[i] = BALL_ID;
+            s.set_q(i, orient);
+        }
+    }
+    if (assigned > 0.f) {
+        s.g_poss = (float)new_team;
+        s.g_inb = 1;
+        s.g_inbclk = 5.f;
+        if (is_oob) s.g_oob += 1.f;
+    }
+}
+
+template <int N>
+BB_HD int offense_index(const World<N> &s)  // game.cpp:1012-1018, 1072-1078
+{
+    int off = 0;
+#pragma unroll
+    for (int i = 1; i < N; i++)
+        if ((float)s.team[i] == s.g_poss) off = i;
+    return off;
+}
+
+// ------------------------------------------------------------------ systems
+template <int N>
+BB_HD void sys_tick(World<N> &s)  // game.cpp:969-988
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        s.rew[i] = 0.f;
+        if (s.rst[i] == 1) { s.done[i] = 1.f; s.step[i] = 0; }
+        else { s.done[i] = 0.f; s.step[i] = s.step[i] + 1u; }
+        s.cd[i] = maxf(0.f, s.cd[i] - 1.f);
+    }
+}
+
+template <int N>
+BB_HD void sys_action_mask(World<N> &s, uint32_t flags)  // game.cpp:489-533
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        int32_t mv = 1, gr = 1, pa = 0, sh = 0;
+        if (s.has[i] == 1) { pa = 1; sh = 1; }
+        if (s.g_inb == 1) {
+            sh = 0; gr = 0;
+            if (s.inb[i] == 1 && s.g_live == 0) mv = 0;
+        }
+        if (s.cd[i] > 0.f) gr = 0;
+        if (!(flags & FLAG_NO_TAG_MASK)) { pa = 0; gr = 0; }
+        s.msk[i][0] = mv; s.msk[i][1] = gr; s.msk[i][2] = pa; s.msk[i][3] = sh;
+    }
+}
+
+template <int N>
+BB_HD void sys_move_agents(World<N> &s, const Ctx &c)  // game.cpp:410-486
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.act[i][2] != 0) {
+            const Q4 turn = quat_axis_z(s.act[i][2] == 1 ? TURN_POS : TURN_NEG, 1.f);
+            s.set_q(i, qmul(turn, s.q(i)));
+        }
+        if (s.msk[i][0] == 0) continue;
+        const float ma = (float)s.act[i][1] * ANGLE_STEP;
+        float sn, cs;
+        bbm::sincosf_(ma, &sn, &cs);
+        F3 dv = (f3(sn, -cs, 0.f) * s.attr[i][1]) * (float)s.act[i][0];
+        float maxs = s.attr[i][0];
+        const F3 fw = forward(s.q(i));
+        F3 v = s.vel(i);
+        float d = 0.f;
+        if (len2(v) > 1e-6f) d = dot(norm(v), fw);
+        if (d < -0.1f) { maxs *= .1f; dv = dv * .1f; }
+        else if (d <= 0.8f) { maxs *= .7f; dv = dv * .1f; }
+        v = v + dv;
+        if (s.has[i] == 1) maxs *= BALL_SLOW;
+        if (len(v) > maxs) v = v * (maxs / len(v));
+        const float dx = v.x * TS, dy = v.y * TS;
+        // the binding's grid is all-empty (src/bindings.cpp:7-11): the wall
+        // lookup of game.cpp:472-484 always accepts the move.
+        s.px[i] = clampf(s.px[i] + dx, 0.f, c.p->width);
+        s.py[i] = clampf(s.py[i] + dy, 0.f, c.p->height);
+        s.set_vel(i, v * .95f);
+    }
+}
+
+template <int N>
+BB_HD void sys_grab(World<N> &s, int i)  // game.cpp:164-239
+{
+    if (s.msk[i][1] == 0 || s.act[i][3] == 0) return;
+    s.cd[i] = 10.f;
+    s.act[i][3] = 0;
+    if (s.fl == 1) return;
+    const int32_t id = AGENT0_ID + i;
+    if (s.has[i] == 1 && s.grab == 1 && s.holder == id) {
+        s.bid[i] = PH; s.has[i] = 0; s.holder = PH; s.grab = 0;
+        return;
+    }
+    if (len(s.bpos() - s.pos(i)) <= 0.3f) {
+        if ((float)s.g_1v1 == 1.f && (float)s.team[i] != s.g_poss) {
+            s.reset_now = 1;
+            return;
+        }
+#pragma unroll
+        for (int j = 0; j < N; j++)
+            if (s.bid[j] == BALL_ID) { s.has[j] = 0; s.bid[j] = PH; s.cd[j] = 62.0f; }
+        s.has[i] = 1; s.bid[i] = BALL_ID;
+        s.holder = id; s.grab = 1; s.fl = 0;
+        s.set_bvel(f3(0.f, 0.f, 0.f));
+        s.sba = PH; s.sbt = PH; s.spv = 2;
+        s.g_poss = (float)s.team[i];
+        s.g_live = 1;
+    }
+}
+
+template <int N>
+BB_HD void sys_pass(World<N> &s, int i)  // game.cpp:243-270
+{
+    if (s.msk[i][2] == 0 || s.act[i][4] == 0) return;
+    if (s.holder == AGENT0_ID + i) {
+        s.grab = 0; s.holder = PH;
+        s.has[i] = 0; s.bid[i] = PH; s.inb[i] = 0;
+        s.set_bvel(rotate(s.q(i), f3(0.f, 0.1f, 0.f)));
+        s.g_inb = 0;
+    }
+}
+
+template <int N>
+BB_HD void sys_shoot(World<N> &s, Ctx &c, int i)  // game.cpp:273-407
+{
+    if (s.msk[i][3] == 0 || s.act[i][5] == 0) return;
+    const F3 pos = s.pos(i);
+    // attacking hoop: the last hoop (creation order) that is not defended
+    F3 target = f3(0.f, 0.f, 0.f);
+    float radius = 0.f;
+    if (HOOP0_ID != s.dhoop[i]) { target = hoop_pos<N>(c, 0); radius = HOOP_ZONE; }
+    if (HOOP1_ID != s.dhoop[i]) { target = hoop_pos<N>(c, 1); radius = HOOP_ZONE; }
+    const F3 ideal = target - pos;
+    const float intended = bbm::atan2f_(ideal.x, ideal.y);
+    const float dstd = DIST_DEV * len(ideal);
+    const float dev_d = sample_uniform(s, c, -dstd, dstd);
+    float dev_def = 0.0f;
+    float nd = __builtin_inff();
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (s.team[j] != s.team[i]) {
+            const float dd = len(pos - s.pos(j));
+            if (dd < nd) nd = dd;
+        }
+    }
+    if (nd < 2.0f) {
+        const float sd = DEF_DEV / (nd + 0.1f);
+        dev_def = sample_uniform(s, c, -sd, sd);
+    }
+    float dev_v = 0.0f;
+    if (s.act[i][0] > 0) {
+        const float sv = VEL_DEV * len(s.vel(i));
+        dev_v = sample_uniform(s, c, -sv, sv);
+    }
+    const float dir = intended + ((dev_d + dev_def) + dev_v);
+    float sn, cs;
+    bbm::sincosf_(dir, &sn, &cs);
+    const F3 fs = f3(sn, cs, 0.f);
+    float going = 0.0f;
+    const float along = dot(ideal, fs);
+    if (!(along < 0.f)) going = (len2(ideal) - along * along <= radius * radius) ? 1.0f : 0.0f;
+    s.set_q(i, rotation_from_forward(fs));
+    if (s.holder == AGENT0_ID + i) {
+        const int32_t v = shot_point_value(pos, target);
+        if (going == 1.f) { s.gin = 1; s.g_bask += 1.f; }
+        else s.rew[i] -= 1.f;
+        s.grab = 0; s.holder = PH;
+        s.has[i] = 0; s.bid[i] = PH; s.inb[i] = 0;
+        s.set_bvel(fs * .1f);
+        s.fl = 1;
+        s.sba = AGENT0_ID + i; s.sbt = s.team[i]; s.spv = v;
+        s.lta = AGENT0_ID + i; s.ltt = s.team[i];
+    }
+}
+
+template <int N>
+BB_HD void sys_move_ball(World<N> &s, const Ctx &c)  // game.cpp:82-125
+{
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (s.has[i] == 1 && s.grab == 1 && s.holder == AGENT0_ID + i) s.set_bpos(s.pos(i));
+    if (len(s.bvel()) == 0.f || s.grab == 1) return;
+    const float nx = clampf(s.bx + s.bvx, 0.f, c.p->width);
+    const float ny = clampf(s.by + s.bvy, 0.f, c.p->height);
+    const float nz = s.bz + s.bvz;
+    s.bx = nx; s.by = ny; s.bz = nz;  // empty grid: never a wall (game.cpp:118-124)
+}
+
+template <int N>
+BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c)  // game.cpp:758-809
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.has[i] == 0) { s.attr[i][8] = 0.f; continue; }
+        const F3 p = s.pos(i);
+        const F3 hoop = (HOOP0_ID != s.dhoop[i]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+        const float dh = len(hoop - p);
+        float nd = __builtin_inff();
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            if (s.team[j] != s.team[i]) {
+                const float dd = len(p - s.pos(j));
+                if (dd < nd) nd = dd;
+            }
+        }
+        const float ds = DIST_DEV * dh;
+        const float fs = DEF_DEV / nd + .0001f;
+        const float vs = VEL_DEV * len(s.vel(i));
+        const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
+        const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
+        s.attr[i][8] = (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)));
+    }
+}
+
+template <int N>
+BB_HD void sys_score(World<N> &s, Ctx &c, int h)  // game.cpp:873-953
+{
+    const F3 hp = hoop_pos<N>(c, h);
+    const int32_t hid = h == 0 ? HOOP0_ID : HOOP1_ID;
+    const float dx = s.bx - hp.x, dy = s.by - hp.y;
+    if (!(bbm::sqrtf_(dx * dx + dy * dy) <= HOOP_ZONE && (float)s.fl == 1.f)) return;
+    const int32_t pts = s.spv;
+    int32_t inb_team = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (s.dhoop[j] == hid) inb_team = s.team[j];
+        if (AGENT0_ID + j == s.sba) {
+            float *st = c.p->c.stats + (c.w * N + j) * 2;
+            st[0] = st[0] + (float)((s.dhoop[j] == hid) ? -s.spv : s.spv);
+        }
+    }
+    F3 spot;
+    if (hid == s.g_h0) { s.g_s1 += (float)pts; spot = f3(CMINX, hp.y + INBOUND_DY, 0.f); }
+    else { s.g_s0 += (float)pts; spot = f3(CMAXX, hp.y + INBOUND_DY, 0.f); }
+    s.g_bask += 1.f;
+    s.fl = 0;
+    s.set_bvel(f3(0.f, 0.f, 0.f));
+    s.sba = PH; s.sbt = PH; s.spv = 2; s.gin = 0;
+    if ((float)s.g_1v1 == 0.f) {
+        s.set_bpos(spot);
+        assign_inbounder(s, spot, inb_team, rotation_from_forward(vec_to_center(c, s.bpos())), false);
+    } else {
+        s.reset_now = 1;
+    }
+}
+
+template <int N>
+BB_HD void sys_out_of_bounds(World<N> &s, Ctx &c)  // game.cpp:1055-1113
+{
+    if (!((s.bx < CMINX || s.bx > CMAXX || s.by < CMINY || s.by > CMAXY) && (float)s.g_inb == 0.f)) return;
+    if ((float)s.g_1v1 == 1.f) {
+        s.rew[offense_index(s)] -= 100.f;
+        s.reset_now = 1;
+        return;
+    }
+    s.fl = 0;
+    s.set_bvel(f3(0.f, 0.f, 0.f));
+    s.g_live = 0;
+    const int32_t new_team = 1 - s.ltt;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.has[i] == 1 && s.bid[i] == BALL_ID) {
+            s.set_pos(i, s.pos(i) + vec_to_center(c, s.pos(i)));
+            s.has[i] = 0; s.bid[i] = PH;
+        }
+    }
+    assign_inbounder(s, s.bpos(), new_team, rotation_from_forward(vec_to_center(c, s.bpos())), true);
+}
+
+template <int N>
+BB_HD void sys_last_touch(World<N> &s)  // game.cpp:1034-1051
+{
+#pragma unroll
+    for (int i = 0; i < N; i++)
+        if (len(s.bpos() - s.pos(i)) <= AGENT_SIZE) { s.lta = AGENT0_ID + i; s.ltt = s.team[i]; }
+}
+
+template <int N>
+BB_HD void sys_clock(World<N> &s)  // game.cpp:992-1030
+{
+    if ((float)s.g_live > 0.5f && s.g_clock > 0.f) { s.g_clock -= TS; s.g_shot -= TS; }
+    if ((float)s.g_inb > 0.5f) s.g_inbclk -= TS;
+    if (s.g_clock <= 0.f && (float)s.g_live > 0.5f) {
+        s.rew[offense_index(s)] += 10.f;
+        s.reset_now = 1;
+    }
+    if (s.g_shot < 0.f) s.g_shot = 0.f;
+}
+
+template <int N>
+BB_HD void sys_inbound_violation(World<N> &s, Ctx &c)  // game.cpp:1116-1157
+{
+    if (!((float)s.g_inb > 0.5f && s.g_inbclk <= 0.f)) return;
+    const int32_t new_team = 1 - (int32_t)s.g_poss;
+    int32_t turn_id = PH;
+    s.g_live = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if ((float)s.inb[i] > 0.5f) {
+            turn_id = s.bid[i];
+            s.inb[i] = 0; s.has[i] = 0; s.bid[i] = PH;
+            s.set_pos(i, s.pos(i) + vec_to_center(c, s.pos(i)));
+        }
+    }
+    if (turn_id != PH && turn_id == BALL_ID) {
+        s.grab = 0; s.holder = PH;
+        assign_inbounder(s, s.bpos(), new_team, rotation_from_forward(vec_to_center(c, s.bpos())), true);
+    }
+}
+
+template <int N>
+BB_HD void sys_points_worth(World<N> &s, const Ctx &c)  // game.cpp:129-161
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        // first hoop (creation order) that is not defended; both are never defended at once
+        if (HOOP0_ID != s.dhoop[i]) s.pw[i] = shot_point_value(s.pos(i), hoop_pos<N>(c, 0));
+        else if (HOOP1_ID != s.dhoop[i]) s.pw[i] = shot_point_value(s.pos(i), hoop_pos<N>(c, 1));
+        else s.pw[i] = 2;
+    }
+}
+
+struct Proj { float mn, mx; };
+BB_HD Proj project(const F3 (&v)[4], F3 axis)  // helper.cpp:85-100
+{
+    Proj p; p.mn = dot(v[0], axis); p.mx = p.mn;
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        const float d = dot(v[k], axis);
+        if (d < p.mn) p.mn = d;
+        if (d > p.mx) p.mx = d;
+    }
+    return p;
+}
+
+// Oriented-rectangle SAT contact between agents a < b (game.cpp:537-648).
+template <int N>
+BB_HD void collide_pair(World<N> &s, int a, int b)
+{
+    const F3 ca = s.pos(a), fa = forward(s.q(a));
+    const F3 ra = f3(fa.y, -fa.x, 0.f);
+    const F3 hwa = ra * HALF_SHOULDER, hda = fa * HALF_DEPTH;
+    const F3 va[4] = {(ca - hda) + hwa, (ca - hda) - hwa, (ca + hda) - hwa, (ca + hda) + hwa};
+    const F3 cb = s.pos(b), fb = forward(s.q(b));
+    const F3 rb = f3(fb.y, -fb.x, 0.f);
+    const F3 hwb = rb * HALF_SHOULDER, hdb = fb * HALF_DEPTH;
+    const F3 vb[4] = {(cb - hdb) + hwb, (cb - hdb) - hwb, (cb + hdb) - hwb, (cb + hdb) + hwb};
+    const F3 axes[4] = {norm(ra), norm(fa), norm(rb), norm(fb)};
+    float min_ov = 3.40282347e+38f;
+    F3 mtv = f3(0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const Proj pa = project(va, axes[k]), pb = project(vb, axes[k]);
+        if (!(pa.mx > pb.mn && pb.mx > pa.mn)) return;  // separating axis
+        const float ov = minf(pa.mx, pb.mx) - maxf(pa.mn, pb.mn);
+        if (ov < min_ov) { min_ov = ov; mtv = axes[k]; }
+    }
+    if (s.g_poss == (float)s.team[a]) {
+        s.rew[a] -= 10.f;
+        s.rew[b] += 10.f;
+        s.reset_now = 1;
+    }
+    F3 corr = mtv;
+    if (dot(cb - ca, corr) < 0.f) corr = -corr;
+    s.set_pos(a, s.pos(a) - (corr * min_ov) * 0.5f);
+    s.set_pos(b, s.pos(b) + (corr * min_ov) * 0.5f);
+}
+
+template <int N>
+BB_HD void sys_collisions(World<N> &s)
+{
+#pragma unroll
+    for (int a = 0; a < N; a++)
+#pragma unroll
+        for (int b = a + 1; b < N; b++) collide_pair(s, a, b);
+}
+
+template <int N>
+BB_HD void sys_defense(World<N> &s, const Ctx &c)  // game.cpp:651-755
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        if (s.g_poss == (float)s.team[i]) { s.act[i][0] = 0; continue; }
+        s.act[i][3] = 1;
+        F3 guard = f3(0.f, 0.f, 0.f);
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            if (s.has[j] == 1 && !found) {
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    if (s.dhoop[i] == (h == 0 ? HOOP0_ID : HOOP1_ID)) {
+                        const F3 hd = hoop_pos<N>(c, h) - s.pos(j);
+                        guard = (len2(hd) > 1e-6f) ? s.pos(j) + norm(hd) * GUARD : s.pos(j);
+                        found = true;
+                    }
+                }
+            }
+        }
+        if (!found) { s.act[i][0] = 0; continue; }
+        const F3 cur = s.target(i);
+        s.set_target(i, cur + (guard - cur) * (s.attr[i][4] * TS));
+        const F3 mv = s.target(i) - s.pos(i);
+        if (len2(mv) < 0.01f) { s.act[i][0] = 0; continue; }
+        // argmax over the 8 move directions of game.cpp:713-722 (first max wins)
+        const F3 desired = norm(mv);
+        const float diag = 1.0f / bbm::sqrtf_(2.f);
+        const float dots[8] = {
+            dot(desired, f3(0.f * 1.f, -1.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, -1.f * diag, 0.f * diag)),
+            dot(desired, f3(1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, 1.f * diag, 0.f * diag)),
+            dot(desired, f3(0.f * 1.f, 1.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, 1.f * diag, 0.f * diag)),
+            dot(desired, f3(-1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, -1.f * diag, 0.f * diag))};
+        float maxd = -2.f;
+        int32_t best = 0;
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (dots[k] > maxd) { maxd = dots[k]; best = k; }
+        s.act[i][0] = 1;
+        s.act[i][1] = best;
+        const F3 fw = forward(s.q(i));
+        const float ang = (float)bbm::acos_d((double)clampf(dot(fw, norm(mv)), -1.f, 1.f));
+        if (ang > PI_OVER_8) {
+            const float cr = fw.x * mv.y - fw.y * mv.x;
+            s.act[i][2] = cr < 0.f ? -1 : (cr > 0.f ? 1 : 0);
+        } else {
+            s.act[i][2] = 0;
+        }
+    }
+}
+
+template <int N>
+BB_HD void sys_reward(World<N> &s)  // game.cpp:811-870
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        const int other = (i == N - 1) ? N - 2 : N - 1;  // last agent != self
+        const float dist = len(s.pos(other) - s.pos(i));
+        if ((float)s.team[i] == s.g_poss) {
+            if (s.g_clock > 5.f) {
+                const int32_t id = AGENT0_ID + i;
+                if (s.sba == id && s.gin == 1) s.rew[i] += (float)s.spv;
+                else if (s.sba == id && s.gin == 0 && s.fl == 1) s.rew[i] -= 1.f;
+                s.rew[i] += s.attr[i][8];
+            }
+        } else {
+            s.rew[i] -= 1.f;
+            s.rew[i] = (float)((double)s.rew[i] + bbm::exp_d((double)(-0.4f * dist)));
+        }
+    }
+}
+
+// ------------------------------------------------------------------ observations
+// fillObservationsSystem (game.cpp:1175-1461).  Values are produced in row
+// order through a sink; with N a compile-time constant every index below
+// folds to a constant and the sink becomes straight-line float4 stores.
+struct RowSink {
+    float *row;
+    float b0, b1, b2, b3;
+    int idx;
+    BB_HD void put(float v)
+    {
+        switch (idx & 3) {
+        case 0: b0 = v; break;
+        case 1: b1 = v; break;
+        case 2: b2 = v; break;
+        default: b3 = v; store_f4(row + (idx & ~3), b0, b1, b2, b3); break;
+        }
+        idx++;
+    }
+    BB_HD void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    BB_HD void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+    // zero-fill up to the next 4-float boundary (the row tail beyond is
+    // zero from construction and never written non-zero)
+    BB_HD void finish() { while (idx & 3) put(0.f); }
+};
+
+// Runtime-indexed sink for the non-canonical team layouts (any Team edits
+// that leave a slot empty or overfull): scalar stores over the whole row.
+struct SlowRowSink {
+    float *row;
+    int idx;
+    BB_HD void put(float v) { row[idx++] = v; }
+    BB_HD void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    BB_HD void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+};
+
+template <int N, class Sink>
+BB_HD void obs_agent_block(const World<N> &s, Sink &o, int j, F3 self_pos, F3 hoop)
+{
+    const F3 pj = s.pos(j), to = pj - self_pos;
+    o.put3(pj);
+    o.put3(len2(to) > 1e-6f ? norm(to) : f3(0.f, 0.f, 0.f));
+    o.put(len(to));
+    const Q4 qj = s.q(j);
+    o.put4(qj);
+    const F3 fw = forward(qj);
+    o.put3(fw);
+    const F3 v = s.vel(j);
+    const bool moving = len2(v) > 1e-6f;
+    o.put3(moving ? norm(v) : f3(0.f, 0.f, 0.f));
+    o.put(len(v));
+    const float d = moving ? dot(norm(v), fw) : 0.f;
+    o.put(d);
+    o.put(d <= 0.8f ? 0.1f : 1.f);
+    const F3 th = hoop - pj;
+    const float dh = len(th);
+    o.put3(dh > 1e-6f ? norm(th) : f3(0.f, 0.f, 0.f));
+    o.put(dh);
+    const F3 tb = s.bpos() - pj;
+    const float db = len(tb);
+    o.put3(db > 1e-6f ? norm(tb) : f3(0.f, 0.f, 0.f));
+    o.put(db);
+    o.put((float)s.inb[j]);
+    o.put(s.cd[j]);
+    o.put(s.attr[j][0]); o.put(s.attr[j][1]); o.put(s.attr[j][2]);
+    o.put(s.attr[j][3]); o.put(s.attr[j][4]); o.put(s.attr[j][8]);
+    o.put((float)s.pw[j]);
+    o.put((float)s.has[j]);
+}
+
+template <int N, class Sink>
+BB_HD void obs_header(const World<N> &s, const Ctx &c, Sink &o, int a, F3 *att, F3 *dfn)
+{
+    o.put(s.g_clock); o.put(s.g_shot); o.put(s.g_period);
+    o.put((float)s.g_inb); o.put(s.g_inbclk);
+    o.put(s.team[a] == 0 ? s.g_s0 : s.g_s1);
+    o.put(s.team[a] == 0 ? s.g_s1 : s.g_s0);
+    o.put3(s.bpos()); o.put3(s.bvel());
+    o.put((float)s.grab); o.put((float)s.fl); o.put((float)s.spv); o.put((float)s.ltt);
+    *att = (HOOP0_ID != s.dhoop[a]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+    *dfn = (HOOP0_ID == s.dhoop[a]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+    o.put3(*att); o.put3(*dfn);
+    // self block (23..60): position, 4 zeros, then the shared agent fields
+    const F3 p = s.pos(a);
+    o.put3(p);
+    o.put3(f3(0.f, 0.f, 0.f));
+    o.put(0.f);
+    const Q4 q = s.q(a);
+    o.put4(q);
+    const F3 fw = forward(q);
+    o.put3(fw);
+    const F3 v = s.vel(a);
+    const bool moving = len2(v) > 1e-6f;
+    o.put3(moving ? norm(v) : f3(0.f, 0.f, 0.f));
+    o.put(len(v));
+    const float d = moving ? dot(norm(v), fw) : 0.f;
+    o.put(d);
+    o.put(d <= 0.8f ? 0.1f : 1.f);
+    const F3 th = *att - p;
+    const float dh = len(th);
+    o.put3(dh > 1e-6f ? norm(th) : f3(0.f, 0.f, 0.f));
+    o.put(dh);
+    const F3 tb = s.bpos() - p;
+    const float db = len(tb);
+    o.put3(db > 1e-6f ? norm(tb) : f3(0.f, 0.f, 0.f));
+    o.put(db);
+    o.put((float)s.inb[a]);
+    o.put(s.cd[a]);
+    o.put(s.attr[a][0]); o.put(s.attr[a][1]); o.put(s.attr[a][2]);
+    o.put(s.attr[a][3]); o.put(s.attr[a][4]); o.put(s.attr[a][8]);
+    o.put((float)s.pw[a]);
+    o.put((float)s.has[a]);
+}
+
+template <int N>
+BB_HD int32_t inbounder_id(const World<N> &s)
+{
+    int32_t id = -1;
+#pragma unroll
+    for (int i = 0; i < N; i++) if ((float)s.inb[i] > 0.5f) id = AGENT0_ID + i;
+    return id;
+}
+
+// true when every other agent fills a slot: exactly N/2-1 teammates and N/2
+// opponents (always the case for the generated i % 2 teams)
+template <int N>
+BB_HD bool canonical_slots(const World<N> &s, int a)
+{
+    int mates = 0, opps = 0;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (j == a) continue;
+        if (s.team[j] == s.team[a]) mates++; else opps++;
+    }
+    return mates == N / 2 - 1 && opps == N / 2;
+}
+
+template <int N>
+BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row)
+{
+    RowSink o;
+    o.row = row; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+    F3 att, dfn;
+    obs_header(s, c, o, a, &att, &dfn);
+    const F3 p = s.pos(a);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (j == a) continue;
+        obs_agent_block(s, o, j, p, s.team[j] == s.team[a] ? att : dfn);
+    }
+    const int32_t ib = inbounder_id(s);
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
+    o.finish();
+}
+
+template <int N>
+BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row)
+{
+    SlowRowSink o;
+    o.row = row; o.idx = 0;
+    F3 att, dfn;
+    obs_header(s, c, o, a, &att, &dfn);
+    const F3 p = s.pos(a);
+    int mates = 0, opps = 0;
+    const int max_mates = N / 2 - 1, max_opps = N / 2;
+    for (int j = 0; j < N; j++) {
+        if (j == a) continue;
+        if (s.team[j] == s.team[a]) {
+            if (mates < max_mates) { obs_agent_block(s, o, j, p, att); mates++; }
+        } else {
+            if (opps < max_opps) { obs_agent_block(s, o, j, p, dfn); opps++; }
+        }
+    }
+    for (int k = mates; k < max_mates; k++) for (int z = 0; z < 37; z++) o.put(0.f);
+    for (int k = opps; k < max_opps; k++) for (int z = 0; z < 37; z++) o.put(0.f);
+    const int32_t ib = inbounder_id(s);
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
+    for (; o.idx < obs_width(N); ) o.put(0.f);
+}
+
+template <int N>
+BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
+{
+#pragma unroll
+    for (int a = 0; a < N; a++) {
+        float *row = c.p->c.obs + (c.w * N + a) * (int64_t)obs_width(N);
+        if (canonical_slots(s, a)) fill_obs_fast(s, c, a, row);
+        else fill_obs_slow(s, c, a, row);
+    }
+}
+
+// ------------------------------------------------------------------ one step
+template <int N>
+BB_HD void step_world(World<N> &s, Ctx &c)
+{
+    const uint32_t flags = c.p->flags;
+    sys_tick(s);                                   // 1
+    sys_action_mask(s, flags);                     // 2
+    sys_move_agents(s, c);                         // 3
+#pragma unroll
+    for (int i = 0; i < N; i++) sys_grab(s, i);    // 4
+#pragma unroll
+    for (int i = 0; i < N; i++) sys_pass(s, i);    // 5
+#pragma unroll
+    for (int i = 0; i < N; i++) sys_shoot(s, c, i);  // 6
+    sys_move_ball(s, c);                           // 7
+    sys_shot_percentage(s, c);                     // 8
+    sys_score(s, c, 0);                            // 9 (hoop 0, then hoop 1)
+    sys_score(s, c, 1);
+    sys_out_of_bounds(s, c);                       // 10
+    sys_last_touch(s);                             // 11
+    sys_clock(s);                                  // 12
+    sys_inbound_violation(s, c);                   // 13
+    if (s.reset_now != 0) {                        // 14 resetSystem
+        reset_world(s, c);
+        s.reset_now = 0;
+    }
+    sys_points_worth(s, c);                        // 15
+    sys_collisions(s);                             // 16
+    sys_defense(s, c);                             // 17
+    sys_fill_obs(s, c);                            // 18
+    sys_reward(s);                                 // 19
+}
+
+// ------------------------------------------------------------------ load/store
+template <int N>
+BB_HD void load_world(World<N> &s, const Params &p, int64_t w)
+{
+    const Columns &c = p.c;
+    {
+        uint32_t g[14];
+        load_words<14>(c.game_state, w, g);
+        s.g_inb = (int32_t)g[0]; s.g_live = (int32_t)g[1]; s.g_period = bitsf(g[2]); s.g_poss = bitsf(g[3]);
+        s.g_h0 = (int32_t)g[4]; s.g_s0 = bitsf(g[5]); s.g_h1 = (int32_t)g[6]; s.g_s1 = bitsf(g[7]);
+        s.g_clock = bitsf(g[8]); s.g_shot = bitsf(g[9]); s.g_bask = bitsf(g[10]); s.g_oob = bitsf(g[11]);
+        s.g_inbclk = bitsf(g[12]); s.g_1v1 = (int32_t)g[13];
+    }
+    s.reset_now = c.world_clock[w];
+    s.rng_ctr = c.rng_counter[w];
+    {
+        uint32_t r[N], a[6 * N], pos[3 * N], ps[3 * N], q[4 * N], v[3 * N], cd[N], st[N], ib[2 * N];
+        uint32_t at[10 * N];
+        load_words<N>(c.reset, w, r);
+        load_words<6 * N>(c.action, w, a);
+        load_words<3 * N>(c.agent_pos, w, pos);
+        load_words<3 * N>(c.possession, w, ps);
+        load_words<4 * N>(c.orientation, w, q);
+        load_words<3 * N>(c.agent_vel, w, v);
+        load_words<N>(c.cooldown, w, cd);
+        load_words<N>(c.cur_step, w, st);
+        load_words<2 * N>(c.inbounding, w, ib);
+        load_words<10 * N>(c.attributes, w, at);
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            s.rst[i] = (int32_t)r[i];
+#pragma unroll
+            for (int k = 0; k < 6; k++) s.act[i][k] = (int32_t)a[6 * i + k];
+            s.px[i] = bitsf(pos[3 * i]); s.py[i] = bitsf(pos[3 * i + 1]); s.pz[i] = bitsf(pos[3 * i + 2]);
+            s.has[i] = (int32_t)ps[3 * i]; s.bid[i] = (int32_t)ps[3 * i + 1]; s.pw[i] = (int32_t)ps[3 * i + 2];
+            s.qw[i] = bitsf(q[4 * i]); s.qx[i] = bitsf(q[4 * i + 1]); s.qy[i] = bitsf(q[4 * i + 2]); s.qz[i] = bitsf(q[4 * i + 3]);
+            s.vx[i] = bitsf(v[3 * i]); s.vy[i] = bitsf(v[3 * i + 1]); s.vz[i] = bitsf(v[3 * i + 2]);
+            s.cd[i] = bitsf(cd[i]);
+            s.step[i] = st[i];
+            s.inb[i] = (int32_t)ib[2 * i]; s.allow[i] = (int32_t)ib[2 * i + 1];
+#pragma unroll
+            for (int k = 0; k < 10; k++) s.attr[i][k] = bitsf(at[10 * i + k]);
+            const uint32_t *t = c.team + (w * N + i) * 5;
+            s.team[i] = (int32_t)t[0];
+            s.dhoop[i] = (int32_t)t[4];
+            // Reward and Done are rewritten by tick before any read; ActionMask
+            // by actionMaskSystem: none of the three is loaded.
+            s.rew[i] = 0.f; s.done[i] = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; k++) s.msk[i][k] = 0;
+        }
+    }
+    {
+        const float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
+        s.bx = bp[0]; s.by = bp[1]; s.bz = bp[2];
+        s.bvx = bv[0]; s.bvy = bv[1]; s.bvz = bv[2];
+        const int32_t *ph = c.ball_physics + w * 7;
+        s.fl = ph[0]; s.lta = ph[1]; s.ltt = ph[2]; s.sba = ph[3]; s.sbt = ph[4]; s.spv = ph[5]; s.gin = ph[6];
+        uint32_t gb[2];
+        load_words<2>(c.ball_grabbed, w, gb);
+        s.grab = (int32_t)gb[0]; s.holder = (int32_t)gb[1];
+    }
+}
+
+template <int N>
+BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
+{
+    const Columns &c = p.c;
+    {
+        const uint32_t g[14] = {(uint32_t)s.g_inb, (uint32_t)s.g_live, fbits(s.g_period), fbits(s.g_poss),
+                                (uint32_t)s.g_h0, fbits(s.g_s0), (uint32_t)s.g_h1, fbits(s.g_s1),
+                                fbits(s.g_clock), fbits(s.g_shot), fbits(s.g_bask), fbits(s.g_oob),
+                                fbits(s.g_inbclk), (uint32_t)s.g_1v1};
+        store_words<14>(c.game_state, w, g);
+    }
+    c.world_clock[w] = s.reset_now;
+    c.rng_counter[w] = s.rng_ctr;
+    uint32_t r[N], a[6 * N], m[4 * N], pos[3 * N], rw[N], dn[N], ps[3 * N], q[4 * N], v[3 * N], cd[N], st[N],
+        ib[2 * N], at[10 * N];
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        r[i] = (uint32_t)s.rst[i];
+#pragma unroll
+        for (int k = 0; k < 6; k++) a[6 * i + k] = (uint32_t)s.act[i][k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) m[4 * i + k] = (uint32_t)s.msk[i][k];
+        pos[3 * i] = fbits(s.px[i]); pos[3 * i + 1] = fbits(s.py[i]); pos[3 * i + 2] = fbits(s.pz[i]);
+        rw[i] = fbits(s.rew[i]); dn[i] = fbits(s.done[i]);
+        ps[3 * i] = (uint32_t)s.has[i]; ps[3 * i + 1] = (uint32_t)s.bid[i]; ps[3 * i + 2] = (uint32_t)s.pw[i];
+        q[4 * i] = fbits(s.qw[i]); q[4 * i + 1] = fbits(s.qx[i]); q[4 * i + 2] = fbits(s.qy[i]); q[4 * i + 3] = fbits(s.qz[i]);
+        v[3 * i] = fbits(s.vx[i]); v[3 * i + 1] = fbits(s.vy[i]); v[3 * i + 2] = fbits(s.vz[i]);
+        cd[i] = fbits(s.cd[i]);
+        st[i] = s.step[i];
+        ib[2 * i] = (uint32_t)s.inb[i]; ib[2 * i + 1] = (uint32_t)s.allow[i];
+#pragma unroll
+        for (int k = 0; k < 10; k++) at[10 * i + k] = fbits(s.attr[i][k]);
+        // Team changes only inside generate/reset, which write it directly.
+    }
+    store_words<N>(c.reset, w, r);
+    store_words<6 * N>(c.action, w, a);
+    store_words<4 * N>(c.action_mask, w, m);
+    store_words<3 * N>(c.agent_pos, w, pos);
+    store_words<N>(c.reward, w, rw);
+    store_words<N>(c.done, w, dn);
+    store_words<3 * N>(c.possession, w, ps);
+    store_words<4 * N>(c.orientation, w, q);
+    store_words<3 * N>(c.agent_vel, w, v);
+    store_words<N>(c.cooldown, w, cd);
+    store_words<N>(c.cur_step, w, st);
+    store_words<2 * N>(c.inbounding, w, ib);
+    store_words<10 * N>(c.attributes, w, at);
+    float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
+    bp[0] = s.bx; bp[1] = s.by; bp[2] = s.bz;
+    bv[0] = s.bvx; bv[1] = s.bvy; bv[2] = s.bvz;
+    int32_t *ph = c.ball_physics + w * 7;
+    ph[0] = s.fl; ph[1] = s.lta; ph[2] = s.ltt; ph[3] = s.sba; ph[4] = s.sbt; ph[5] = s.spv; ph[6] = s.gin;
+    const uint32_t gb[2] = {(uint32_t)s.grab, (uint32_t)s.holder};
+    store_words<2>(c.ball_grabbed, w, gb);
+}
+
+// Constant columns written once at construction: entity ids, hoop positions.
+template <int N>
+BB_HD void init_static_columns(const Params &p, int64_t w)
+{
+#pragma unroll
+    for (int i = 0; i < N; i++) p.c.agent_id[w * N + i] = AGENT0_ID + i;
+    p.c.ball_id[w] = BALL_ID;
+    float *h = p.c.hoop_pos + w * 6;
+    h[0] = p.hoop0[0]; h[1] = p.hoop0[1]; h[2] = p.hoop0[2];
+    h[3] = p.hoop1[0]; h[4] = p.hoop1[1]; h[5] = p.hoop1[2];
+}
+
+// World generation into the columns (obs rows zeroed).
+template <int N>
+BB_HD void init_world(const Params &p, int64_t w)
+{
+    World<N> s;
+    Ctx c; c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    generate_world(s, c);
+    store_world(s, p, w);
+    init_static_columns<N>(p, w);
+    float *o = p.c.obs + w * N * (int64_t)obs_width(N);
+    for (int k = 0; k < N * obs_width(N); k++) o[k] = 0.f;
+}
+
+template <int N>
+BB_HD void step_one_world(const Params &p, int64_t w)
+{
+    World<N> s;
+    load_world(s, p, w);
+    Ctx c; c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    step_world(s, c);
+    store_world(s, p, w);
+}
+
+}  // namespace bb
