@@ -1,0 +1,176 @@
+"""Throughput benchmark of the MI355X basketball step (BASELINE.json metric).
+
+python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds 65536] [--agents 2]
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+A "step" = the synthetic random-action write (the stand-in for the Python
+`actions[:] = ...` of scripts/env.py:147) + one step of every world on this
+GPU, both on-device with inputs resident in HBM.  Worlds are sharded across
+ranks (weak scaling: --worlds per GPU); there is no collective on the step
+path, only a barrier and a max-reduce of the elapsed time around the timed
+region.  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "env steps/sec (whole node) at 65 536 worlds; 1→8 GPU scaling"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(num_agents: int, seconds: float):
+    """The oracle (a single-threaded C restatement of the reference's CPU
+    executor) on a bounded sample of the same workload."""
+    from oracle.oracle import Oracle
+    from oracle import oracle as O
+    W = 4096
+    o = Oracle(W, num_agents=num_agents, flags=O.FLAG_PER_WORLD_RNG)
+    o.run_random(5, 321, 0)  # warm
+    steps, elapsed = 0, 0.0
+    while elapsed < seconds:
+        elapsed += o.run_random(10, 321, 5 + steps)
+        steps += 10
+    return {"value": W * steps / elapsed, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{W} worlds x {steps} steps, {num_agents} agents, threefry random actions, "
+                      f"single thread ({elapsed:.1f} s)"}
+
+
+def load_traffic(workload_key: str):
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return d.get(workload_key)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--worlds", type=int, default=65536, help="worlds per GPU")
+    ap.add_argument("--agents", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=321)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    import madrona_basketball_amd as mba
+    from madrona_basketball_amd import _lib
+
+    W = args.worlds
+    sim = mba.SimpleGridworldSimulator(
+        discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
+        max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W, gpu_id=dev.index,
+        num_agents=args.agents, per_world_rng=True, world_offset=rank * W)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if world_size > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    def max_over_ranks(x: float) -> float:
+        if world_size == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # warmup (untimed)
+    sim.step_n(args.warmup, random_actions=True, action_seed=args.seed, step0=0)
+    barrier()
+
+    # timed region: exactly K steps
+    t0 = time.perf_counter()
+    sim.step_n(args.steps, random_actions=True, action_seed=args.seed, step0=args.warmup)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    barrier()
+    elapsed = max_over_ranks(elapsed)
+
+    # kernel timing (HIP events around every step kernel, same stream)
+    kernel_ms = sim.step_n(args.steps, random_actions=True, action_seed=args.seed,
+                           step0=args.warmup + args.steps, time_kernels=True)
+    barrier()
+    avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / args.steps)
+
+    total_worlds = W * world_size
+    value = total_worlds * args.steps / elapsed
+    bytes_per_launch = _lib.load().bb_algorithmic_bytes_per_world(args.agents) * W
+    achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
+    workload_key = f"W{W}_N{args.agents}"
+    traffic = load_traffic(workload_key)
+
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "env-steps/s",
+        "n_gpus": world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {
+            "workload": f"{W} worlds per GPU x {args.agents} agents (reference 1v1 game, "
+                        f"NUM_AGENTS={args.agents}), threefry random actions each step (buckets "
+                        f"[2,8,3,2,2,2]), per-world RNG",
+            "worlds_per_gpu": W,
+            "total_worlds": total_worlds,
+            "agents_per_world": args.agents,
+            "parallelism": f"world-sharded x{world_size}, no collectives on the step path",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "bb::k_step<%d>" % args.agents,
+            "kernel_avg_us": avg_kernel_s * 1e6,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+        },
+    }
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.agents, args.cpu_seconds)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world_size > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,63 @@
+#!/bin/bash
+# One gpurun call: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a fault/abort/timeout (exit >= 124,
+# 134, 139, or a signal) ends the script immediately.  Ordinary test failures
+# (exit 1) are recorded and the remaining steps still run.
+# Usage: bash tools/gpu_round.sh [tag] [steps...]   steps: smoke tests bench prof pmc
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-smoke tests bench prof}
+ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd "$ROOT"
+export PYTHONUNBUFFERED=1
+
+fatal() {  # exit codes that mean the GPU step did not end normally
+    local rc=$1
+    [ "$rc" -eq 0 ] && return 1
+    [ "$rc" -eq 1 ] && return 1   # pytest: tests failed
+    [ "$rc" -eq 2 ] && return 1   # pytest: interrupted/usage
+    [ "$rc" -eq 5 ] && return 1   # pytest: nothing collected
+    return 0
+}
+
+run() {  # name timeout cmd...
+    local name=$1 tmo=$2
+    shift 2
+    echo "=== $name ($(date +%T))" | tee -a "$OUT/summary.txt"
+    timeout -k 10 "$tmo" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a "$OUT/summary.txt"
+    tail -n 5 "$OUT/$name.log" | tee -a "$OUT/summary.txt"
+    if fatal $rc; then
+        echo "FATAL: $name ended with $rc; stopping" | tee -a "$OUT/summary.txt"
+        exit $rc
+    fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+    smoke) run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rA ;;
+    bench) run bench 600 python bench.py --steps 1000 --warmup 100 ;;
+    bench262k) run bench262k 600 python bench.py --worlds 262144 --steps 500 --warmup 50 --no-cpu-baseline ;;
+    bench8k) run bench8k 600 python bench.py --worlds 8192 --steps 1000 --warmup 100 --no-cpu-baseline ;;
+    bench4) run bench4 600 python bench.py --agents 4 --steps 500 --warmup 50 --no-cpu-baseline ;;
+    bench10) run bench10 600 python bench.py --agents 10 --steps 200 --warmup 20 --no-cpu-baseline ;;
+    prof)
+        ( cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps 300 --warmup 30 --no-cpu-baseline ) || exit $?
+        ;;
+    pmc)
+        ( cd /tmp && export TMPDIR=/tmp && run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline ) || exit $?
+        ( cd /tmp && export TMPDIR=/tmp && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline ) || exit $?
+        ;;
+    *) echo "unknown step $s" ;;
+    esac
+done
+echo "=== done" | tee -a "$OUT/summary.txt"
