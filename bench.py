@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--seed", type=int, default=321)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
+                    help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
 
     import torch
@@ -74,12 +76,17 @@ def main():
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    on_gpu = args.exec == "cuda"
+    if on_gpu:
+        torch.cuda.set_device(local_rank if world_size > 1 else 0)
+        dev = torch.device("cuda", torch.cuda.current_device())
     else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+        dev = torch.device("cpu")
+    if world_size > 1:
+        if on_gpu:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     import madrona_basketball_amd as mba
     from madrona_basketball_amd import _lib
@@ -87,14 +94,19 @@ def main():
     W = args.worlds
     sim = mba.SimpleGridworldSimulator(
         discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
-        max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W, gpu_id=dev.index,
+        max_episode_length=39600, exec_mode=mba.ExecMode.CUDA if on_gpu else mba.ExecMode.CPU,
+        num_worlds=W, gpu_id=dev.index if on_gpu else -1,
         num_agents=args.agents, per_world_rng=True, world_offset=rank * W)
 
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize(dev)
+
     def barrier():
-        torch.cuda.synchronize(dev)
+        sync()
         if world_size > 1:
             dist.barrier()
-        torch.cuda.synchronize(dev)
+        sync()
 
     def max_over_ranks(x: float) -> float:
         if world_size == 1:
@@ -110,16 +122,19 @@ def main():
     # timed region: exactly K steps
     t0 = time.perf_counter()
     sim.step_n(args.steps, random_actions=True, action_seed=args.seed, step0=args.warmup)
-    torch.cuda.synchronize(dev)
+    sync()
     elapsed = time.perf_counter() - t0
     barrier()
     elapsed = max_over_ranks(elapsed)
 
     # kernel timing (HIP events around every step kernel, same stream)
-    kernel_ms = sim.step_n(args.steps, random_actions=True, action_seed=args.seed,
-                           step0=args.warmup + args.steps, time_kernels=True)
-    barrier()
-    avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / args.steps)
+    if on_gpu:
+        kernel_ms = sim.step_n(args.steps, random_actions=True, action_seed=args.seed,
+                               step0=args.warmup + args.steps, time_kernels=True)
+        barrier()
+        avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / args.steps)
+    else:
+        avg_kernel_s = elapsed / args.steps
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
@@ -162,6 +177,9 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },
     }
+    if not on_gpu:
+        out["roofline"] = None
+        out["config"]["parallelism"] += " (host executor, gloo)"
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.agents, args.cpu_seconds)
     elif rank == 0:

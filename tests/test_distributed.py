@@ -1,0 +1,79 @@
+"""Multi-rank path on CPU with gloo (world_size 2): bench.py's launch and
+max-over-ranks timing, and world sharding = unsharded results."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _libs(native_lib, oracle_lib):
+    pass
+
+
+def test_bench_two_ranks_gloo():
+    port = free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", BB_CPU_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--exec", "cpu", "--worlds", "512", "--steps", "20", "--warmup", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_worlds"] == 1024 and out["value"] > 0
+    assert out["scaling"] == "weak" and out["steps"] == 20
+
+
+def _worker(rank, world, port, W, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    shard = W // world
+    sim = make_sim(ExecMode.CPU, shard, per_world_rng=True, world_offset=rank * shard)
+    sim.step_n(steps, random_actions=True, action_seed=5)
+    obs = sim.observations_tensor().to_torch().contiguous()
+    gathered = [torch.empty_like(obs) for _ in range(world)]
+    dist.all_gather(gathered, obs)
+    if rank == 0:
+        q.put(torch.cat(gathered).numpy())
+    dist.destroy_process_group()
+
+
+def test_sharded_ranks_equal_single_process():
+    W, steps = 128, 150
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, steps, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    full = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    full.step_n(steps, random_actions=True, action_seed=5)
+    assert np.array_equal(got.view(np.uint32), full.observations_tensor().to_torch().numpy().view(np.uint32))
