@@ -13,7 +13,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIB_NAME = "libmadrona_basketball_amd.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
-SOURCES = ["bb_kernels.hip", "bb_host.hip"]
+AGENT_COUNTS = [2, 4, 6, 8, 10]
+# (source, extra flags, object name): the step kernel once per agent count,
+# compiled in parallel
+UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}"], f"bb_kernels_n{n}.o") for n in AGENT_COUNTS]
+         + [("bb_common.hip", [], "bb_common.o"), ("bb_host.hip", [], "bb_host.o")])
+SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["bb_math.h", "bb_rng.h", "bb_sim.h", "bb_launch.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 
@@ -50,13 +55,18 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     build_dir = os.path.join(HERE, "_build")
     os.makedirs(build_dir, exist_ok=True)
-    for src in SOURCES:
-        obj = os.path.join(build_dir, src.replace(".hip", ".o"))
-        cmd = [cc, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
-        if verbose:
-            print(" ".join(cmd), file=sys.stderr)
-        subprocess.run(cmd, check=True)
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = max(1, min(len(UNITS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
+    cmds = []
+    for src, extra, objname in UNITS:
+        obj = os.path.join(build_dir, objname)
+        cmds.append([cc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
+        if verbose:
+            print(" ".join(cmds[-1]), file=sys.stderr)
+    with ThreadPoolExecutor(jobs) as ex:
+        for r in ex.map(lambda c: subprocess.run(c), cmds):
+            r.check_returncode()
     tmp = LIB_PATH + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:

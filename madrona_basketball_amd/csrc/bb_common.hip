@@ -1,0 +1,96 @@
+// bb_common.hip -- small kernels shared by every agent count: the synthetic
+// action workload, device-side pokes (set_action / trigger_reset), a
+// streaming probe for roofline calibration, and the N dispatch.
+#include <hip/hip_runtime.h>
+#include "bb_launch.h"
+#include "bb_rng.h"
+
+namespace bb {
+
+// one lane = one (world, agent) action row (24 B)
+__global__ __launch_bounds__(256) void k_random_actions(int32_t *action, int64_t rows, int32_t n,
+                                                        int64_t world_offset, uint32_t seed, uint32_t step)
+{
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= rows) return;
+    const int64_t w = r / n;
+    const int32_t a = (int32_t)(r - w * n);
+    int32_t act[6];
+    random_action(seed, step, (uint32_t)(world_offset + w), (uint32_t)a, act);
+    int2 *dst = (int2 *)(action + r * 6);
+    dst[0] = make_int2(act[0], act[1]);
+    dst[1] = make_int2(act[2], act[3]);
+    dst[2] = make_int2(act[4], act[5]);
+}
+
+struct Poke { int32_t v[16]; };
+__global__ void k_poke(int32_t *dst, int32_t count, Poke vals)
+{
+    const int k = threadIdx.x;
+    if (k < count) dst[k] = vals.v[k];
+}
+
+// Coalesced streaming probe: item i reads read_q float4 and writes write_q
+// float4, laid out [q][item] so every wave instruction is 1 KiB contiguous.
+__global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= items) return;
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = 0; q < read_q; q++) {
+        const float4 v = src[(int64_t)q * items + i];
+        acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    for (int q = 0; q < write_q; q++) dst[(int64_t)q * items + i] = acc;
+}
+
+static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
+
+hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s)
+{
+    const int64_t rows = p.num_worlds * n;
+    hipLaunchKernelGGL(k_random_actions, grid_for(rows, 256), dim3(256), 0, s, p.c.action, rows, n,
+                       p.world_offset, seed, step);
+    return hipGetLastError();
+}
+
+hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s)
+{
+    if (count < 0 || count > 16) return hipErrorInvalidValue;
+    Poke pk;
+    for (int k = 0; k < 16; k++) pk.v[k] = k < count ? vals[k] : 0;
+    hipLaunchKernelGGL(k_poke, dim3(1), dim3(64), 0, s, dst, count, pk);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, hipStream_t s)
+{
+    hipLaunchKernelGGL(k_stream_probe, grid_for(items, 256), dim3(256), 0, s, src, dst, items, read_q, write_q);
+    return hipGetLastError();
+}
+
+#define BB_DISPATCH_N(n, call)                  \
+    switch (n) {                                \
+    case 2: return call(2);                     \
+    case 4: return call(4);                     \
+    case 6: return call(6);                     \
+    case 8: return call(8);                     \
+    case 10: return call(10);                   \
+    default: return hipErrorInvalidValue;       \
+    }
+
+hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode)
+{
+#define CALL(k) launch_step_t<k>(p, mode, s)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
+hipError_t launch_init(int n, const Params &p, hipStream_t s)
+{
+#define CALL(k) launch_init_t<k>(p, s)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
+}  // namespace bb

@@ -188,6 +188,7 @@ void bind_params(bb_sim *s)
     p.hoop1[0] = csx + bb::COURT_L - bb::HOOP_FROM_BASE; p.hoop1[1] = ccy; p.hoop1[2] = 0.f;
     p.seed = cfg.rand_seed;
     p.flags = cfg.flags;
+    bb::build_tables(p);
 }
 
 int64_t slot_bytes(const bb_config *cfg, int id)
@@ -543,6 +544,47 @@ int bb_export(bb_sim *s, int32_t export_id, void **ptr, int32_t *dtype, int32_t 
 int64_t bb_num_worlds(const bb_sim *s) { return s ? s->cfg.num_worlds : 0; }
 int32_t bb_num_agents(const bb_sim *s) { return s ? s->n : 0; }
 int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
+
+// Diagnostic (not in the public header): average ms of `iters` back-to-back
+// launches of a k_step variant (bb::StepMode) or, for mode 100, of a
+// coalesced streaming probe moving read_q/write_q 16-byte pieces per world.
+int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t write_q, void *stream,
+                 float *avg_ms)
+{
+    if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || iters < 1 || !avg_ms) return fail(BB_ERR_INVALID_ARG, "bb_diag_time");
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    float4 *src = nullptr, *dst = nullptr;
+    const int64_t W = s->cfg.num_worlds;
+    if (mode == 100) {
+        if (hipMalloc(&src, (size_t)W * read_q * 16) != hipSuccess || hipMalloc(&dst, (size_t)W * write_q * 16) != hipSuccess)
+            return fail(BB_ERR_OOM, "probe buffers");
+        (void)hipMemsetAsync(src, 0, (size_t)W * read_q * 16, st);
+    }
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    auto once = [&]() -> hipError_t {
+        if (mode == 100) return bb::launch_stream_probe(src, dst, W, read_q, write_q, st);
+        return bb::launch_step(s->n, s->p, st, mode);
+    };
+    hipError_t e = once();  // warm
+    if (e == hipSuccess) {
+        (void)hipEventRecord(e0, st);
+        for (int k = 0; k < iters && e == hipSuccess; k++) e = once();
+        (void)hipEventRecord(e1, st);
+        (void)hipEventSynchronize(e1);
+    }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (src) (void)hipFree(src);
+    if (dst) (void)hipFree(dst);
+    if (e != hipSuccess) return hip_fail(e, "diag launch");
+    *avg_ms = ms / iters;
+    return BB_OK;
+}
 
 int64_t bb_algorithmic_bytes_per_world(int32_t n)
 {

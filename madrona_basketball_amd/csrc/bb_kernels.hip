@@ -1,102 +1,120 @@
-// bb_kernels.hip -- gfx950 kernels of the basketball step.
+// bb_kernels.hip -- gfx950 step kernel of the basketball simulator; compiled
+// once per agent count (-DBB_N=2,4,6,8,10).
 //
-// k_step<N>: one lane = one world.  The lane loads its world's columns
-// (16/8-byte vector loads where the per-world chunk allows), runs the 19
-// systems of src/game.cpp:1463-1526 on registers (bb_sim.h), and writes the
-// columns back; observation rows are written as float4 stores.  Replaces the
-// reference's 19 ParallelFor megakernel nodes + 3 sort nodes per step
-// (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
+// k_step<N>: one lane = one world, one wave = one workgroup of 64 worlds.
+//   1. the lane loads its world's columns (16/8-byte vector loads where the
+//      per-world chunk allows) into a register-resident World<N>;
+//   2. systems 1-17 of src/game.cpp:1463-1526 run on registers (bb_sim.h);
+//   3. fillObservations (game.cpp:1175-1461): for each agent slot the lane
+//      writes its row into an LDS tile (conflict-free ds_write_b128, row
+//      stride 4 mod 8 dwords), then the wave stores the 64 rows back as
+//      consecutive 16-byte pieces, so every 1 KiB store instruction covers
+//      whole 128-byte lines instead of 64 scattered ones;
+//   4. rewardSystem, then every modified column is stored.
+// Replaces the reference's 19 ParallelFor megakernel nodes + 3 sort nodes per
+// step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
-#include "bb_sim.h"
 #include "bb_launch.h"
+#include "bb_sim.h"
+
+#ifndef BB_N
+#error "compile bb_kernels.hip with -DBB_N=<agents>"
+#endif
 
 namespace bb {
 
-constexpr int STEP_BLOCK = 256;
+constexpr int WAVE = 64;
 
 template <int N>
-__global__ __launch_bounds__(STEP_BLOCK) void k_step(const Params p)
+struct ObsTile {
+    static constexpr int QW = (obs_used(N) + 3) / 4;  // float4 pieces of a used row
+    static constexpr int RS = QW * 4 + 4;             // LDS row stride (floats): == 4 mod 8
+    // LDS-staged rows only while the tile leaves room for >= 2 waves per CU
+    static constexpr bool STAGED = (WAVE * RS * 4) <= 64 * 1024;
+    static constexpr int FLOATS = STAGED ? WAVE * RS : 4;
+};
+
+template <int N, int MODE>
+__global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
-    const int64_t w = (int64_t)blockIdx.x * STEP_BLOCK + threadIdx.x;
-    if (w >= p.num_worlds) return;
-    step_one_world<N>(p, w);
+    using T = ObsTile<N>;
+    __shared__ float4 tile4[T::FLOATS / 4];
+    float *tile = (float *)tile4;
+    const int lane = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t w = w0 + lane;
+    const bool active = w < p.num_worlds;
+
+    World<N> s;
+    Ctx c;
+    c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    if (active) {
+        load_world(s, p, w);
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
+    }
+    if constexpr (MODE == MODE_IO) {
+        if (active) store_world(s, p, w);
+        return;
+    }
+    if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
+        if (active) sys_fill_obs(s, c);
+    } else if constexpr (MODE != MODE_NO_OBS) {
+        constexpr int OW = obs_width(N);
+#pragma unroll
+        for (int a = 0; a < N; a++) {
+            const bool fast = active && canonical_slots(s, a);
+            if (fast) fill_obs_fast(s, c, a, tile + lane * T::RS);
+            else if (active) fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW);
+            __syncthreads();
+            const uint64_t staged = __ballot(fast);
+            float *obs_a = p.c.obs + (w0 * N + a) * (int64_t)OW;
+            for (int f = lane; f < WAVE * T::QW; f += WAVE) {
+                const int r = f / T::QW, q = f - r * T::QW;
+                if ((staged >> r) & 1ull) {
+                    const float4 v = *(const float4 *)(tile + r * T::RS + 4 * q);
+                    *(float4 *)(obs_a + (int64_t)r * N * OW + 4 * q) = v;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (active) {
+        if constexpr (MODE != MODE_IO_OBS) sys_reward(s);
+        store_world(s, p, w);
+    }
 }
 
 template <int N>
-__global__ __launch_bounds__(STEP_BLOCK) void k_init(const Params p)
+__global__ __launch_bounds__(256) void k_init(const Params p)
 {
-    const int64_t w = (int64_t)blockIdx.x * STEP_BLOCK + threadIdx.x;
+    const int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (w >= p.num_worlds) return;
     init_world<N>(p, w);
 }
 
-// one lane = one (world, agent) action row (24 B)
-__global__ __launch_bounds__(256) void k_random_actions(int32_t *action, int64_t rows, int32_t n,
-                                                        int64_t world_offset, uint32_t seed,
-                                                        uint32_t step)
-{
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (r >= rows) return;
-    const int64_t w = r / n;
-    const int32_t a = (int32_t)(r - w * n);
-    int32_t act[6];
-    random_action(seed, step, (uint32_t)(world_offset + w), (uint32_t)a, act);
-    int2 *dst = (int2 *)(action + r * 6);
-    dst[0] = make_int2(act[0], act[1]);
-    dst[1] = make_int2(act[2], act[3]);
-    dst[2] = make_int2(act[4], act[5]);
-}
-
-struct Poke { int32_t v[8]; };
-__global__ void k_poke(int32_t *dst, int32_t count, Poke vals)
-{
-    const int k = threadIdx.x;
-    if (k < count) dst[k] = vals.v[k];
-}
-
-static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
-
 template <int N>
-static hipError_t launch_step_n(const Params &p, hipStream_t s)
+hipError_t launch_step_t(const Params &p, int mode, hipStream_t s)
 {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N>), grid_for(p.num_worlds, STEP_BLOCK), dim3(STEP_BLOCK), 0, s, p);
-    return hipGetLastError();
-}
-
-template <int N>
-static hipError_t launch_init_n(const Params &p, hipStream_t s)
-{
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_init<N>), grid_for(p.num_worlds, STEP_BLOCK), dim3(STEP_BLOCK), 0, s, p);
-    return hipGetLastError();
-}
-
-#define BB_DISPATCH_N(n, fn, ...)                       \
-    switch (n) {                                        \
-    case 2: return fn<2>(__VA_ARGS__);                  \
-    case 4: return fn<4>(__VA_ARGS__);                  \
-    case 6: return fn<6>(__VA_ARGS__);                  \
-    case 8: return fn<8>(__VA_ARGS__);                  \
-    case 10: return fn<10>(__VA_ARGS__);                \
-    default: return hipErrorInvalidValue;               \
+    const dim3 grid((unsigned)((p.num_worlds + WAVE - 1) / WAVE)), block(WAVE);
+    switch (mode) {
+    case MODE_FULL: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_FULL>), grid, block, 0, s, p); break;
+    case MODE_IO: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO>), grid, block, 0, s, p); break;
+    case MODE_IO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO_OBS>), grid, block, 0, s, p); break;
+    case MODE_DIRECT_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_DIRECT_OBS>), grid, block, 0, s, p); break;
+    case MODE_NO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_NO_OBS>), grid, block, 0, s, p); break;
+    default: return hipErrorInvalidValue;
     }
-
-hipError_t launch_step(int n, const Params &p, hipStream_t s) { BB_DISPATCH_N(n, launch_step_n, p, s) }
-hipError_t launch_init(int n, const Params &p, hipStream_t s) { BB_DISPATCH_N(n, launch_init_n, p, s) }
-
-hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s)
-{
-    const int64_t rows = p.num_worlds * n;
-    hipLaunchKernelGGL(k_random_actions, grid_for(rows, 256), dim3(256), 0, s, p.c.action, rows, n,
-                       p.world_offset, seed, step);
     return hipGetLastError();
 }
 
-hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s)
+template <int N>
+hipError_t launch_init_t(const Params &p, hipStream_t s)
 {
-    Poke pk;
-    for (int k = 0; k < 8; k++) pk.v[k] = k < count ? vals[k] : 0;
-    hipLaunchKernelGGL(k_poke, dim3(1), dim3(64), 0, s, dst, count, pk);
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_init<N>), dim3((unsigned)((p.num_worlds + 255) / 256)), dim3(256), 0, s, p);
     return hipGetLastError();
 }
+
+template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t);
+template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 
 }  // namespace bb

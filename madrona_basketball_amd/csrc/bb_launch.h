@@ -1,17 +1,42 @@
-// bb_launch.h -- host-side entry points into the gfx950 kernels (bb_kernels.hip)
-// and the host executor (bb_host.hip).
+// bb_launch.h -- host-side entry points into the gfx950 kernels
+// (bb_kernels.hip, one translation unit per agent count) and the host executor.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "bb_sim.h"
 
 namespace bb {
 
-hipError_t launch_step(int n, const Params &p, hipStream_t s);
+// Kernel variants of k_step (diagnostics for the roofline analysis; MODE_FULL
+// is the product kernel).
+enum StepMode : int {
+    MODE_FULL = 0,        // 19 systems, observation rows staged through LDS
+    MODE_IO = 1,          // load + store of every column only
+    MODE_IO_OBS = 2,      // load + observation rows + store, no systems
+    MODE_DIRECT_OBS = 3,  // 19 systems, observation rows stored lane-strided (v1)
+    MODE_NO_OBS = 4,      // systems 1-17 and 19, no observation rows
+};
+
+template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s);
+template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
+
+#define BB_EXTERN_N(n)                                                                  \
+    extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t);      \
+    extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);
+BB_EXTERN_N(2)
+BB_EXTERN_N(4)
+BB_EXTERN_N(6)
+BB_EXTERN_N(8)
+BB_EXTERN_N(10)
+#undef BB_EXTERN_N
+
+hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL);
 hipError_t launch_init(int n, const Params &p, hipStream_t s);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);
+// streaming copy with the step's traffic mix (read_b, write_b bytes per item)
+hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, hipStream_t s);
 
-// Host executor (ExecMode.CPU): the same step_one_world<N> over a thread pool.
+// Host executor (ExecMode.CPU): the same step code over a thread pool.
 int host_step(int n, const Params &p, int threads);
 int host_init(int n, const Params &p);
 int host_random_actions(int n, const Params &p, uint32_t seed, uint32_t step);

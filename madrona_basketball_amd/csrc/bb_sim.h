@@ -184,6 +184,13 @@ struct Params {
     float width, height, start_x, start_y;
     float hoop0[3], hoop1[3];
     uint32_t seed, flags;
+    // Derived tables, computed once on the host with the very functions the
+    // step would call (so a table hit is bit-identical to the evaluation):
+    float mv_sin[8], mv_cos[8];  // sincos((float)k * pi/4), k = moveAngle in [0, 8)
+    Q4 turn_q[2];                // angleAxis(+6 deg, z), angleAxis(-6 deg, z)   game.cpp:423-424
+    Q4 start_q[2];               // angleAxis(-pi/2, z), angleAxis(+pi/2, z)     gen.cpp:196
+    float rot_thresh;            // (float)acos(c) > pi/8  <=>  c < rot_thresh   game.cpp:746-747
+    int32_t rot_exact;           // 1: threshold not verified, evaluate acos
 };
 
 BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
@@ -245,6 +252,33 @@ BB_HD void store_f4(float *p, float a, float b, float c, float d)
 #else
     p[0] = a; p[1] = b; p[2] = c; p[3] = d;
 #endif
+}
+
+// Fill the derived tables of Params (host).  Every entry is produced by the
+// same deterministic function the step would evaluate.
+inline bool rot_pred(float c) { return (float)bbm::acos_d((double)c) > PI_OVER_8; }
+
+inline void build_tables(Params &p)
+{
+    for (int k = 0; k < 8; k++) bbm::sincosf_((float)k * ANGLE_STEP, &p.mv_sin[k], &p.mv_cos[k]);
+    p.turn_q[0] = quat_axis_z(TURN_POS, 1.f);
+    p.turn_q[1] = quat_axis_z(TURN_NEG, 1.f);
+    p.start_q[0] = quat_axis_z(-PI / 2.0f, 1.f);  // == start_orientation_eval(0)
+    p.start_q[1] = quat_axis_z(PI / 2.0f, 1.f);   // == start_orientation_eval(1)
+    // bisection over float bit patterns in [0.5, 1]: pred(lo) true, pred(hi) false
+    uint32_t lo = fbits(0.5f), hi = fbits(1.0f);
+    if (!rot_pred(bitsf(lo)) || rot_pred(bitsf(hi))) { p.rot_exact = 1; p.rot_thresh = 0.f; return; }
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (rot_pred(bitsf(mid))) lo = mid; else hi = mid;
+    }
+    p.rot_thresh = bitsf(hi);
+    p.rot_exact = 0;
+    // verify c < T  <=>  pred(c) on a window of 2^17 floats around T
+    for (int64_t k = -65536; k <= 65536; k++) {
+        const float cval = bitsf((uint32_t)((int64_t)hi + k));
+        if (rot_pred(cval) != (cval < p.rot_thresh)) { p.rot_exact = 1; return; }
+    }
 }
 
 // ------------------------------------------------------------------ state
@@ -320,10 +354,15 @@ BB_HD F3 vec_to_center(const Ctx &c, F3 p)  // findVectorToCenter, helper.cpp:44
 }
 
 // ------------------------------------------------------------------ gen/reset
-template <int N>
-BB_HD Q4 start_orientation(int i)  // gen.cpp:196 / :277
+BB_HD Q4 start_orientation_eval(int i)  // gen.cpp:196 / :277
 {
     return (i % 2 == 0) ? quat_axis_z(-PI / 2.0f, 1.f) : quat_axis_z(PI / 2.0f, 1.f);
+}
+
+template <int N>
+BB_HD Q4 start_orientation(const Ctx &c, int i)
+{
+    return c.p->start_q[i % 2];
 }
 
 // setupAgentPositions (src/helper.cpp:108-160); returns the ball holder id.
@@ -399,7 +438,7 @@ BB_HD void generate_world(World<N> &s, Ctx &c)
 #pragma unroll
         for (int k = 0; k < 4; k++) s.msk[i][k] = 0;
         s.rst[i] = 0; s.inb[i] = 0; s.allow[i] = 1; s.rew[i] = 0.f; s.done[i] = 0.f; s.step[i] = 0;
-        s.set_q(i, start_orientation<N>(i));
+        s.set_q(i, start_orientation<N>(c, i));
         s.cd[i] = 0.f;
         s.vx[i] = 0.f; s.vy[i] = 0.f; s.vz[i] = 0.f;
         s.team[i] = i % 2;
@@ -437,7 +476,7 @@ BB_HD void reset_world(World<N> &s, Ctx &c)
 #pragma unroll
         for (int k = 0; k < 4; k++) s.msk[i][k] = 0;
         s.rst[i] = 0; s.inb[i] = 0; s.allow[i] = 1; s.done[i] = 1.f; s.step[i] = 0;
-        s.set_q(i, start_orientation<N>(i));
+        s.set_q(i, start_orientation<N>(c, i));
         s.cd[i] = 0.f;
         s.vx[i] = 0.f; s.vy[i] = 0.f; s.vz[i] = 0.f;
         s.team[i] = i % 2;
@@ -526,13 +565,19 @@ BB_HD void sys_move_agents(World<N> &s, const Ctx &c)  // game.cpp:410-486
 #pragma unroll
     for (int i = 0; i < N; i++) {
         if (s.act[i][2] != 0) {
-            const Q4 turn = quat_axis_z(s.act[i][2] == 1 ? TURN_POS : TURN_NEG, 1.f);
+            const Q4 turn = s.act[i][2] == 1 ? c.p->turn_q[0] : c.p->turn_q[1];
             s.set_q(i, qmul(turn, s.q(i)));
         }
         if (s.msk[i][0] == 0) continue;
-        const float ma = (float)s.act[i][1] * ANGLE_STEP;
-        float sn, cs;
-        bbm::sincosf_(ma, &sn, &cs);
+        const int32_t m = s.act[i][1];
+        float sn = c.p->mv_sin[0], cs = c.p->mv_cos[0];
+        if ((uint32_t)m < 8u) {
+#pragma unroll
+            for (int k = 1; k < 8; k++)
+                if (m == k) { sn = c.p->mv_sin[k]; cs = c.p->mv_cos[k]; }
+        } else {
+            bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
+        }
         F3 dv = (f3(sn, -cs, 0.f) * s.attr[i][1]) * (float)s.act[i][0];
         float maxs = s.attr[i][0];
         const F3 fw = forward(s.q(i));
@@ -892,8 +937,10 @@ BB_HD void sys_defense(World<N> &s, const Ctx &c)  // game.cpp:651-755
         s.act[i][0] = 1;
         s.act[i][1] = best;
         const F3 fw = forward(s.q(i));
-        const float ang = (float)bbm::acos_d((double)clampf(dot(fw, norm(mv)), -1.f, 1.f));
-        if (ang > PI_OVER_8) {
+        const float cosang = clampf(dot(fw, norm(mv)), -1.f, 1.f);
+        const bool turn = c.p->rot_exact ? ((float)bbm::acos_d((double)cosang) > PI_OVER_8)
+                                         : (cosang < c.p->rot_thresh);
+        if (turn) {
             const float cr = fw.x * mv.y - fw.y * mv.x;
             s.act[i][2] = cr < 0.f ? -1 : (cr > 0.f ? 1 : 0);
         } else {
@@ -1118,8 +1165,9 @@ BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
 }
 
 // ------------------------------------------------------------------ one step
+// Systems 1-17 (everything before fillObservations).
 template <int N>
-BB_HD void step_world(World<N> &s, Ctx &c)
+BB_HD void step_world_pre_obs(World<N> &s, Ctx &c)
 {
     const uint32_t flags = c.p->flags;
     sys_tick(s);                                   // 1
@@ -1146,6 +1194,12 @@ BB_HD void step_world(World<N> &s, Ctx &c)
     sys_points_worth(s, c);                        // 15
     sys_collisions(s);                             // 16
     sys_defense(s, c);                             // 17
+}
+
+template <int N>
+BB_HD void step_world(World<N> &s, Ctx &c)
+{
+    step_world_pre_obs(s, c);                      // 1-17
     sys_fill_obs(s, c);                            // 18
     sys_reward(s);                                 // 19
 }

@@ -1,0 +1,60 @@
+"""Time k_step variants (bb::StepMode) and a coalesced streaming probe with the
+same per-world traffic, interleaved in one process (guide §5.4 rule 24).
+
+python tools/ablate.py [--worlds 65536] [--agents 2] [--iters 200] [--rounds 5]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+MODES = {0: "full (LDS-staged obs)", 1: "io only", 2: "io + obs rows", 3: "full (lane-strided obs, v1)",
+         4: "full minus obs", 100: "stream probe (same bytes, coalesced)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", type=int, default=65536)
+    ap.add_argument("--agents", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    import madrona_basketball_amd as mba
+    from madrona_basketball_amd import _lib
+    L = _lib.load()
+    L.bb_diag_time.restype = ctypes.c_int
+    L.bb_diag_time.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                               ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
+    sim = mba.SimpleGridworldSimulator(32, 17, 15.7575, 8.382, 39600, mba.ExecMode.CUDA, args.worlds, 0,
+                                       num_agents=args.agents, per_world_rng=True)
+    sim.step_n(50, random_actions=True)  # realistic, diverged state
+    torch.cuda.synchronize()
+    B = L.bb_algorithmic_bytes_per_world(args.agents)
+    read_q, write_q = 28, (B * 0 + 1256 + 15) // 16
+    res = {m: [] for m in MODES}
+    stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for r in range(args.rounds):
+        for m in MODES:
+            ms = ctypes.c_float()
+            rc = L.bb_diag_time(sim._h, m, args.iters, read_q, write_q, stream, ctypes.byref(ms))
+            assert rc == 0, L.bb_last_error()
+            res[m].append(ms.value * 1e3)
+    out = {}
+    for m, v in res.items():
+        med = statistics.median(v)
+        out[MODES[m]] = {"median_us": med, "min_us": min(v), "algorithmic_GBps": B * args.worlds / (med * 1e-6) / 1e9}
+        print(f"{MODES[m]:40s} median {med:8.2f} us  min {min(v):8.2f} us  "
+              f"alg {out[MODES[m]]['algorithmic_GBps']:7.0f} GB/s", flush=True)
+    print(json.dumps({"worlds": args.worlds, "agents": args.agents, "results": out}))
+
+
+if __name__ == "__main__":
+    main()

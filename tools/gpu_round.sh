@@ -47,6 +47,8 @@ for s in $STEPS; do
     bench8k) run bench8k 600 python bench.py --worlds 8192 --steps 1000 --warmup 100 --no-cpu-baseline ;;
     bench4) run bench4 600 python bench.py --agents 4 --steps 500 --warmup 50 --no-cpu-baseline ;;
     bench10) run bench10 600 python bench.py --agents 10 --steps 200 --warmup 20 --no-cpu-baseline ;;
+    ablate) run ablate 600 python tools/ablate.py --worlds 65536 ;;
+    ablate262k) run ablate262k 600 python tools/ablate.py --worlds 262144 --iters 50 ;;
     prof)
         ( cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
             --output-format csv -- python3 "$ROOT/bench.py" --steps 300 --warmup 30 --no-cpu-baseline ) || exit $?
