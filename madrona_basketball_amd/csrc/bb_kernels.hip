@@ -1,16 +1,19 @@
 // bb_kernels.hip -- gfx950 step kernel of the basketball simulator; compiled
 // once per agent count (-DBB_N=2,4,6,8,10).
 //
-// k_step<N>: one lane = one world, one wave = one workgroup of 64 worlds.
-//   1. the lane loads its world's columns (16/8-byte vector loads where the
+// k_step<N>: one wave = one 64-lane workgroup; at N = 2 and 4 one lane per
+// agent (64/N worlds per wave), otherwise one lane per world.
+//   1. every lane loads its world's columns (16/8-byte vector loads where the
 //      per-world chunk allows) into a register-resident World<N>;
-//   2. systems 1-17 of src/game.cpp:1463-1526 run on registers (bb_sim.h);
-//   3. fillObservations (game.cpp:1175-1461): for each agent slot the lane
-//      writes its row into an LDS tile (conflict-free ds_write_b128, row
-//      stride 4 mod 8 dwords), then the wave stores the 64 rows back as
-//      consecutive 16-byte pieces, so every 1 KiB store instruction covers
-//      whole 128-byte lines instead of 64 scattered ones;
-//   4. rewardSystem, then every modified column is stored.
+//   2. systems 1-17 of src/game.cpp:1463-1526 run on registers (bb_sim.h),
+//      identically in the N lanes of a world;
+//   3. fillObservations (game.cpp:1175-1461): each lane writes its agent's
+//      row into an LDS tile (conflict-free ds_write_b128, row stride 4 mod 8
+//      dwords); the wave then stores the 64 rows -- consecutive in memory --
+//      as consecutive 16-byte pieces (whole 128-byte lines per instruction
+//      instead of 64 scattered ones);
+//   4. rewardSystem for the lane's agent, then the lane stores its agent's
+//      columns and the agent-0 lane the world columns.
 // Replaces the reference's 19 ParallelFor megakernel nodes + 3 sort nodes per
 // step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
@@ -34,52 +37,93 @@ struct ObsTile {
     static constexpr int FLOATS = STAGED ? WAVE * RS : 4;
 };
 
+// Lanes per world: with one lane per agent (N = 2, 4) the lanes of a world
+// all hold the full world state and run systems 1-17 identically, but each
+// computes and stores only its own agent's observation row, reward and
+// per-agent columns; the world-level columns are stored by the agent-0 lane.
+template <int N>
+struct Lanes {
+    static constexpr int LPW = (N == 2 || N == 4) ? N : 1;
+    static constexpr int WPB = WAVE / LPW;  // worlds per 64-lane workgroup
+};
+
+// Copy the wave's 64 staged rows (tile row r -> obs row base_row + r*stride)
+// as consecutive 16-byte pieces; rows whose bit is clear in `staged` were
+// written directly (generic layout) or belong to no world.
+template <int N>
+__device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, int64_t row_stride,
+                                           uint64_t staged, int lane)
+{
+    using T = ObsTile<N>;
+    constexpr int OW = obs_width(N);
+    for (int f = lane; f < WAVE * T::QW; f += WAVE) {
+        const int r = f / T::QW, q = f - r * T::QW;
+        if ((staged >> r) & 1ull) {
+            const float4 v = *(const float4 *)(tile + r * T::RS + 4 * q);
+            *(float4 *)(obs + (row0 + (int64_t)r * row_stride) * OW + 4 * q) = v;
+        }
+    }
+}
+
 template <int N, int MODE>
 __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
     using T = ObsTile<N>;
+    constexpr int LPW = Lanes<N>::LPW, WPB = Lanes<N>::WPB;
+    constexpr int OW = obs_width(N);
     __shared__ float4 tile4[T::FLOATS / 4];
     float *tile = (float *)tile4;
     const int lane = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * WAVE;
-    const int64_t w = w0 + lane;
+    const int k = lane % LPW;  // this lane's agent when LPW == N
+    const int64_t w0 = (int64_t)blockIdx.x * WPB;
+    const int64_t w = w0 + lane / LPW;
     const bool active = w < p.num_worlds;
 
     World<N> s;
-    Ctx c;
-    c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    Ctx c = make_ctx(p, w, k == 0);
     if (active) {
         load_world(s, p, w);
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
-    if constexpr (MODE == MODE_IO) {
-        if (active) store_world(s, p, w);
-        return;
-    }
-    if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
+    // ---------------------------------------------------------- observations
+    if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
+        // no observation rows
+    } else if constexpr (LPW == N) {
+        float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
+        if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
+            if (active) {
+                if (canonical_slots(s, k)) fill_obs_fast(s, c, k, grow);
+                else fill_obs_slow(s, c, k, grow);
+            }
+        } else {
+            const bool fast = active && canonical_slots(s, k);
+            if (fast) fill_obs_fast(s, c, k, tile + lane * T::RS);
+            else if (active) fill_obs_slow(s, c, k, grow);
+            __syncthreads();
+            // lane = (w - w0) * N + k: the wave's rows are consecutive in memory
+            flush_tile<N>(tile, p.c.obs, w0 * N, 1, __ballot(fast), lane);
+        }
+    } else if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
         if (active) sys_fill_obs(s, c);
-    } else if constexpr (MODE != MODE_NO_OBS) {
-        constexpr int OW = obs_width(N);
+    } else {
 #pragma unroll
         for (int a = 0; a < N; a++) {
             const bool fast = active && canonical_slots(s, a);
             if (fast) fill_obs_fast(s, c, a, tile + lane * T::RS);
             else if (active) fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW);
             __syncthreads();
-            const uint64_t staged = __ballot(fast);
-            float *obs_a = p.c.obs + (w0 * N + a) * (int64_t)OW;
-            for (int f = lane; f < WAVE * T::QW; f += WAVE) {
-                const int r = f / T::QW, q = f - r * T::QW;
-                if ((staged >> r) & 1ull) {
-                    const float4 v = *(const float4 *)(tile + r * T::RS + 4 * q);
-                    *(float4 *)(obs_a + (int64_t)r * N * OW + 4 * q) = v;
-                }
-            }
+            flush_tile<N>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
             __syncthreads();
         }
     }
-    if (active) {
-        if constexpr (MODE != MODE_IO_OBS) sys_reward(s);
+    // ---------------------------------------------------------- reward + store
+    if (!active) return;
+    if constexpr (LPW == N) {
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(s, k);
+        store_world_agent(s, p, w, k);
+        if (k == 0) store_world_shared(s, p, w);
+    } else {
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);
         store_world(s, p, w);
     }
 }
@@ -95,7 +139,8 @@ __global__ __launch_bounds__(256) void k_init(const Params p)
 template <int N>
 hipError_t launch_step_t(const Params &p, int mode, hipStream_t s)
 {
-    const dim3 grid((unsigned)((p.num_worlds + WAVE - 1) / WAVE)), block(WAVE);
+    constexpr int WPB = Lanes<N>::WPB;
+    const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
     switch (mode) {
     case MODE_FULL: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_FULL>), grid, block, 0, s, p); break;
     case MODE_IO: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO>), grid, block, 0, s, p); break;

@@ -5,11 +5,10 @@
 // This build defines it as threefry2x32-20 (Salmon et al., SC'11; the
 // Random123 / JAX known-answer vectors are checked in tests/test_oracle.py):
 //
-//   world key   = threefry(key = {seed, 0}, ctr = {k, 0}),
-//                 k = 0 for every world (reference-compatible: every world's
-//                 rng is split_i(initKey(0), 0, 0)), or k = global world index
-//                 with BB_FLAG_PER_WORLD_RNG;
-//   draw j      = threefry(world key, {j, 0}).x;  U = (draw >> 8) * 2^-24.
+//   world key   = {seed, k}, k = 0 for every world (reference-compatible:
+//                 every world's rng is split_i(initKey(0), 0, 0)), or k = the
+//                 global world index with BB_FLAG_PER_WORLD_RNG;
+//   draw j      = threefry(world key, ctr = {j, 0}).x;  U = (draw >> 8) * 2^-24.
 //
 // sampleUniform(min, max) = min + (max - min) * U  (src/helper.cpp:8-11).
 #pragma once

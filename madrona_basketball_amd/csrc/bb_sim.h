@@ -323,20 +323,22 @@ struct World {
 struct Ctx {
     const Params *p;
     int64_t w;
-    uint32_t k0, k1;
-    bool key_ready;
+    bool writer;   // this lane performs the world's memory side effects
 };
+
+BB_HD Ctx make_ctx(const Params &p, int64_t w, bool writer = true)
+{
+    Ctx c; c.p = &p; c.w = w; c.writer = writer; return c;
+}
 
 template <int N>
 BB_HD float sample_uniform(World<N> &s, Ctx &c, float lo, float hi)
 {
-    if (!c.key_ready) {
-        const uint32_t idx = (c.p->flags & FLAG_PER_WORLD_RNG) ? (uint32_t)(c.p->world_offset + c.w) : 0u;
-        threefry2x32(c.p->seed, 0u, idx, 0u, &c.k0, &c.k1);
-        c.key_ready = true;
-    }
+    // world key {seed, k}: k = 0 for every world (reference: one shared key,
+    // src/sim.cpp:89) or the global world index (per-world streams)
+    const uint32_t k = (c.p->flags & FLAG_PER_WORLD_RNG) ? (uint32_t)(c.p->world_offset + c.w) : 0u;
     uint32_t r0, r1;
-    threefry2x32(c.k0, c.k1, s.rng_ctr, 0u, &r0, &r1);
+    threefry2x32(c.p->seed, k, s.rng_ctr, 0u, &r0, &r1);
     s.rng_ctr++;
     return lo + (hi - lo) * u01_from_bits(r0);
 }
@@ -445,10 +447,12 @@ BB_HD void generate_world(World<N> &s, Ctx &c)
         s.dhoop[i] = (i % 2 == 0) ? s.g_h0 : s.g_h1;
         s.has[i] = 0; s.bid[i] = 0; s.pw[i] = 0;
         s.px[i] = 0.f; s.py[i] = 0.f; s.pz[i] = 0.f;
-        write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(128.f, 0.f, 128.f),
-                      s.dhoop[i]);
-        float *st = c.p->c.stats + (c.w * N + i) * 2;
-        st[0] = 0.f; st[1] = 0.f;
+        if (c.writer) {
+            write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(128.f, 0.f, 128.f),
+                          s.dhoop[i]);
+            float *st = c.p->c.stats + (c.w * N + i) * 2;
+            st[0] = 0.f; st[1] = 0.f;
+        }
     }
     F3 ball_at = f3(c.p->start_x, c.p->start_y, 0.f);
     const int32_t off_id = setup_agent_positions(s, c, &ball_at);
@@ -481,10 +485,12 @@ BB_HD void reset_world(World<N> &s, Ctx &c)
         s.vx[i] = 0.f; s.vy[i] = 0.f; s.vz[i] = 0.f;
         s.team[i] = i % 2;
         s.dhoop[i] = (i % 2 == 0) ? s.g_h0 : s.g_h1;
-        write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(255.f, 0.f, 100.f),
-                      s.dhoop[i]);
-        float *st = c.p->c.stats + (c.w * N + i) * 2;
-        st[0] = 0.f; st[1] = 0.f;
+        if (c.writer) {
+            write_team<N>(c, i, s.team[i], (i % 2 == 0) ? f3(0.f, 100.f, 255.f) : f3(255.f, 0.f, 100.f),
+                          s.dhoop[i]);
+            float *st = c.p->c.stats + (c.w * N + i) * 2;
+            st[0] = 0.f; st[1] = 0.f;
+        }
     }
     F3 ball_at = f3(c.p->start_x, c.p->start_y, 0.f);
     const int32_t off_id = setup_agent_positions(s, c, &ball_at);
@@ -743,7 +749,7 @@ BB_HD void sys_score(World<N> &s, Ctx &c, int h)  // game.cpp:873-953
 #pragma unroll
     for (int j = 0; j < N; j++) {
         if (s.dhoop[j] == hid) inb_team = s.team[j];
-        if (AGENT0_ID + j == s.sba) {
+        if (AGENT0_ID + j == s.sba && c.writer) {
             float *st = c.p->c.stats + (c.w * N + j) * 2;
             st[0] = st[0] + (float)((s.dhoop[j] == hid) ? -s.spv : s.spv);
         }
@@ -950,24 +956,28 @@ BB_HD void sys_defense(World<N> &s, const Ctx &c)  // game.cpp:651-755
 }
 
 template <int N>
-BB_HD void sys_reward(World<N> &s)  // game.cpp:811-870
+BB_HD void sys_reward_agent(World<N> &s, int i)  // game.cpp:811-870
+{
+    const int other = (i == N - 1) ? N - 2 : N - 1;  // last agent != self
+    const float dist = len(s.pos(other) - s.pos(i));
+    if ((float)s.team[i] == s.g_poss) {
+        if (s.g_clock > 5.f) {
+            const int32_t id = AGENT0_ID + i;
+            if (s.sba == id && s.gin == 1) s.rew[i] += (float)s.spv;
+            else if (s.sba == id && s.gin == 0 && s.fl == 1) s.rew[i] -= 1.f;
+            s.rew[i] += s.attr[i][8];
+        }
+    } else {
+        s.rew[i] -= 1.f;
+        s.rew[i] = (float)((double)s.rew[i] + bbm::exp_d((double)(-0.4f * dist)));
+    }
+}
+
+template <int N>
+BB_HD void sys_reward(World<N> &s)
 {
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        const int other = (i == N - 1) ? N - 2 : N - 1;  // last agent != self
-        const float dist = len(s.pos(other) - s.pos(i));
-        if ((float)s.team[i] == s.g_poss) {
-            if (s.g_clock > 5.f) {
-                const int32_t id = AGENT0_ID + i;
-                if (s.sba == id && s.gin == 1) s.rew[i] += (float)s.spv;
-                else if (s.sba == id && s.gin == 0 && s.fl == 1) s.rew[i] -= 1.f;
-                s.rew[i] += s.attr[i][8];
-            }
-        } else {
-            s.rew[i] -= 1.f;
-            s.rew[i] = (float)((double)s.rew[i] + bbm::exp_d((double)(-0.4f * dist)));
-        }
-    }
+    for (int i = 0; i < N; i++) sys_reward_agent(s, i);
 }
 
 // ------------------------------------------------------------------ observations
@@ -1268,53 +1278,18 @@ BB_HD void load_world(World<N> &s, const Params &p, int64_t w)
     }
 }
 
+// World-level columns (GameState, WorldClock, RNG counter, ball).
 template <int N>
-BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
+BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w)
 {
     const Columns &c = p.c;
-    {
-        const uint32_t g[14] = {(uint32_t)s.g_inb, (uint32_t)s.g_live, fbits(s.g_period), fbits(s.g_poss),
-                                (uint32_t)s.g_h0, fbits(s.g_s0), (uint32_t)s.g_h1, fbits(s.g_s1),
-                                fbits(s.g_clock), fbits(s.g_shot), fbits(s.g_bask), fbits(s.g_oob),
-                                fbits(s.g_inbclk), (uint32_t)s.g_1v1};
-        store_words<14>(c.game_state, w, g);
-    }
+    const uint32_t g[14] = {(uint32_t)s.g_inb, (uint32_t)s.g_live, fbits(s.g_period), fbits(s.g_poss),
+                            (uint32_t)s.g_h0, fbits(s.g_s0), (uint32_t)s.g_h1, fbits(s.g_s1),
+                            fbits(s.g_clock), fbits(s.g_shot), fbits(s.g_bask), fbits(s.g_oob),
+                            fbits(s.g_inbclk), (uint32_t)s.g_1v1};
+    store_words<14>(c.game_state, w, g);
     c.world_clock[w] = s.reset_now;
     c.rng_counter[w] = s.rng_ctr;
-    uint32_t r[N], a[6 * N], m[4 * N], pos[3 * N], rw[N], dn[N], ps[3 * N], q[4 * N], v[3 * N], cd[N], st[N],
-        ib[2 * N], at[10 * N];
-#pragma unroll
-    for (int i = 0; i < N; i++) {
-        r[i] = (uint32_t)s.rst[i];
-#pragma unroll
-        for (int k = 0; k < 6; k++) a[6 * i + k] = (uint32_t)s.act[i][k];
-#pragma unroll
-        for (int k = 0; k < 4; k++) m[4 * i + k] = (uint32_t)s.msk[i][k];
-        pos[3 * i] = fbits(s.px[i]); pos[3 * i + 1] = fbits(s.py[i]); pos[3 * i + 2] = fbits(s.pz[i]);
-        rw[i] = fbits(s.rew[i]); dn[i] = fbits(s.done[i]);
-        ps[3 * i] = (uint32_t)s.has[i]; ps[3 * i + 1] = (uint32_t)s.bid[i]; ps[3 * i + 2] = (uint32_t)s.pw[i];
-        q[4 * i] = fbits(s.qw[i]); q[4 * i + 1] = fbits(s.qx[i]); q[4 * i + 2] = fbits(s.qy[i]); q[4 * i + 3] = fbits(s.qz[i]);
-        v[3 * i] = fbits(s.vx[i]); v[3 * i + 1] = fbits(s.vy[i]); v[3 * i + 2] = fbits(s.vz[i]);
-        cd[i] = fbits(s.cd[i]);
-        st[i] = s.step[i];
-        ib[2 * i] = (uint32_t)s.inb[i]; ib[2 * i + 1] = (uint32_t)s.allow[i];
-#pragma unroll
-        for (int k = 0; k < 10; k++) at[10 * i + k] = fbits(s.attr[i][k]);
-        // Team changes only inside generate/reset, which write it directly.
-    }
-    store_words<N>(c.reset, w, r);
-    store_words<6 * N>(c.action, w, a);
-    store_words<4 * N>(c.action_mask, w, m);
-    store_words<3 * N>(c.agent_pos, w, pos);
-    store_words<N>(c.reward, w, rw);
-    store_words<N>(c.done, w, dn);
-    store_words<3 * N>(c.possession, w, ps);
-    store_words<4 * N>(c.orientation, w, q);
-    store_words<3 * N>(c.agent_vel, w, v);
-    store_words<N>(c.cooldown, w, cd);
-    store_words<N>(c.cur_step, w, st);
-    store_words<2 * N>(c.inbounding, w, ib);
-    store_words<10 * N>(c.attributes, w, at);
     float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
     bp[0] = s.bx; bp[1] = s.by; bp[2] = s.bz;
     bv[0] = s.bvx; bv[1] = s.bvy; bv[2] = s.bvz;
@@ -1322,6 +1297,48 @@ BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
     ph[0] = s.fl; ph[1] = s.lta; ph[2] = s.ltt; ph[3] = s.sba; ph[4] = s.sbt; ph[5] = s.spv; ph[6] = s.gin;
     const uint32_t gb[2] = {(uint32_t)s.grab, (uint32_t)s.holder};
     store_words<2>(c.ball_grabbed, w, gb);
+}
+
+// Per-agent columns of agent i (row w*N + i of every [W][N][...] column).
+// Team changes only inside generate/reset, which write it directly.
+template <int N>
+BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t w, int i)
+{
+    const Columns &c = p.c;
+    const int64_t r = w * N + i;
+    uint32_t a[6], m[4], pos[3], ps[3], q[4], v[3], ib[2], at[10];
+#pragma unroll
+    for (int k = 0; k < 6; k++) a[k] = (uint32_t)s.act[i][k];
+#pragma unroll
+    for (int k = 0; k < 4; k++) m[k] = (uint32_t)s.msk[i][k];
+    pos[0] = fbits(s.px[i]); pos[1] = fbits(s.py[i]); pos[2] = fbits(s.pz[i]);
+    ps[0] = (uint32_t)s.has[i]; ps[1] = (uint32_t)s.bid[i]; ps[2] = (uint32_t)s.pw[i];
+    q[0] = fbits(s.qw[i]); q[1] = fbits(s.qx[i]); q[2] = fbits(s.qy[i]); q[3] = fbits(s.qz[i]);
+    v[0] = fbits(s.vx[i]); v[1] = fbits(s.vy[i]); v[2] = fbits(s.vz[i]);
+    ib[0] = (uint32_t)s.inb[i]; ib[1] = (uint32_t)s.allow[i];
+#pragma unroll
+    for (int k = 0; k < 10; k++) at[k] = fbits(s.attr[i][k]);
+    c.reset[r] = s.rst[i];
+    store_words<6>(c.action, r, a);
+    store_words<4>(c.action_mask, r, m);
+    store_words<3>(c.agent_pos, r, pos);
+    c.reward[r] = s.rew[i];
+    c.done[r] = s.done[i];
+    store_words<3>(c.possession, r, ps);
+    store_words<4>(c.orientation, r, q);
+    store_words<3>(c.agent_vel, r, v);
+    c.cooldown[r] = s.cd[i];
+    c.cur_step[r] = s.step[i];
+    store_words<2>(c.inbounding, r, ib);
+    store_words<10>(c.attributes, r, at);
+}
+
+template <int N>
+BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
+{
+    store_world_shared(s, p, w);
+#pragma unroll
+    for (int i = 0; i < N; i++) store_world_agent(s, p, w, i);
 }
 
 // Constant columns written once at construction: entity ids, hoop positions.
@@ -1341,7 +1358,7 @@ template <int N>
 BB_HD void init_world(const Params &p, int64_t w)
 {
     World<N> s;
-    Ctx c; c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    Ctx c = make_ctx(p, w);
     generate_world(s, c);
     store_world(s, p, w);
     init_static_columns<N>(p, w);
@@ -1354,7 +1371,7 @@ BB_HD void step_one_world(const Params &p, int64_t w)
 {
     World<N> s;
     load_world(s, p, w);
-    Ctx c; c.p = &p; c.w = w; c.key_ready = false; c.k0 = c.k1 = 0;
+    Ctx c = make_ctx(p, w);
     step_world(s, c);
     store_world(s, p, w);
 }

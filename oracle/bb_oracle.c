@@ -12,8 +12,9 @@
  * Build-defined Madrona details (unpinned, the reference's submodule is absent):
  *   - entity ids: hoop0=0, hoop1=1, ball=2, agent i = 3+i (creation order);
  *   - Vector3::normalize(v) = v * (1.0f / sqrtf(v.length2()));
- *   - RNG: threefry2x32-20; world key = tf(initKey={seed,0}, {0 | world, 0});
- *     draw k of a world: U = (tf(worldKey, {k, 0}).x >> 8) * 2^-24.
+ *   - RNG: threefry2x32-20; world key = {seed, 0} (every world, as the
+ *     reference's shared split_i(initKey(0),0,0)) or {seed, global world};
+ *     draw j of a world: U = (tf(worldKey, {j, 0}).x >> 8) * 2^-24.
  */
 #define _POSIX_C_SOURCE 199309L
 #include "bb_oracle.h"
@@ -266,13 +267,11 @@ static void generate_world(OWorld *w, int64_t global_index) /* gen.cpp:13-214 + 
     w->gs.clock = K_TIME_PER_PERIOD; w->gs.shot = 24.f; w->gs.baskets = 0.f; w->gs.oob = 0.f;
     w->gs.inb_clock = 0.f; w->gs.one_v_one = (G->flags & OR_FLAG_FULL_GAME) ? 0 : 1;
     w->reset_now = 0;
-    /* Sim::Sim: rng = split_i(initKey(seed), 0, 0) for every world. */
-    {
-        uint32_t o[2];
-        uint32_t idx = (G->flags & OR_FLAG_PER_WORLD_RNG) ? (uint32_t)global_index : 0u;
-        oracle_threefry2x32(G->cfg.seed, 0u, idx, 0u, o);
-        w->key0 = o[0]; w->key1 = o[1]; w->ctr = 0;
-    }
+    /* Sim::Sim: rng = split_i(initKey(seed), 0, 0) for every world; build
+     * definition: key {seed, 0} (or {seed, global world index}). */
+    w->key0 = G->cfg.seed;
+    w->key1 = (G->flags & OR_FLAG_PER_WORLD_RNG) ? (uint32_t)global_index : 0u;
+    w->ctr = 0;
     float csx = (G->width - K_COURT_L) / 2.0f;
     float ccy = G->height / 2.0f;
     w->hoop[0].id = 0; w->gs.h0 = 0;
