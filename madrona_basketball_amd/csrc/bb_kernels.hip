@@ -86,19 +86,27 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
     // ---------------------------------------------------------- observations
+    // view of the world with this lane's agent in slot 0 (LPW == N)
+    World<N> v;
+    int32_t ib = -1;
+    if constexpr (LPW == N) {
+        if (active) {
+            ib = inbounder_id(s);
+            agent_view(s, v, k);
+        }
+    }
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
-        // no observation rows
     } else if constexpr (LPW == N) {
         float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
         if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
             if (active) {
-                if (canonical_slots(s, k)) fill_obs_fast(s, c, k, grow);
-                else fill_obs_slow(s, c, k, grow);
+                if (canonical_slots(v, 0)) fill_obs_fast(v, c, 0, grow, ib);
+                else fill_obs_slow(v, c, 0, grow, ib);
             }
         } else {
-            const bool fast = active && canonical_slots(s, k);
-            if (fast) fill_obs_fast(s, c, k, tile + lane * T::RS);
-            else if (active) fill_obs_slow(s, c, k, grow);
+            const bool fast = active && canonical_slots(v, 0);
+            if (fast) fill_obs_fast(v, c, 0, tile + lane * T::RS, ib);
+            else if (active) fill_obs_slow(v, c, 0, grow, ib);
             __syncthreads();
             // lane = (w - w0) * N + k: the wave's rows are consecutive in memory
             flush_tile<N>(tile, p.c.obs, w0 * N, 1, __ballot(fast), lane);
@@ -106,11 +114,12 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
     } else if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
         if (active) sys_fill_obs(s, c);
     } else {
+        const int32_t ib1 = active ? inbounder_id(s) : -1;
 #pragma unroll
         for (int a = 0; a < N; a++) {
             const bool fast = active && canonical_slots(s, a);
-            if (fast) fill_obs_fast(s, c, a, tile + lane * T::RS);
-            else if (active) fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW);
+            if (fast) fill_obs_fast(s, c, a, tile + lane * T::RS, ib1);
+            else if (active) fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW, ib1);
             __syncthreads();
             flush_tile<N>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
             __syncthreads();
@@ -119,8 +128,8 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
     // ---------------------------------------------------------- reward + store
     if (!active) return;
     if constexpr (LPW == N) {
-        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(s, k);
-        store_world_agent(s, p, w, k);
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
+        store_world_agent(v, p, w * N + k, 0);
         if (k == 0) store_world_shared(s, p, w);
     } else {
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);

@@ -956,13 +956,14 @@ BB_HD void sys_defense(World<N> &s, const Ctx &c)  // game.cpp:651-755
 }
 
 template <int N>
-BB_HD void sys_reward_agent(World<N> &s, int i)  // game.cpp:811-870
+BB_HD void sys_reward_agent(World<N> &s, int i, int32_t id)  // game.cpp:811-870
 {
-    const int other = (i == N - 1) ? N - 2 : N - 1;  // last agent != self
+    // `other` = the last agent (creation order) that is not self; with slot i
+    // the first of the others ascending (permuted view) this is slot N-1 too
+    const int other = (i == N - 1) ? N - 2 : N - 1;
     const float dist = len(s.pos(other) - s.pos(i));
     if ((float)s.team[i] == s.g_poss) {
         if (s.g_clock > 5.f) {
-            const int32_t id = AGENT0_ID + i;
             if (s.sba == id && s.gin == 1) s.rew[i] += (float)s.spv;
             else if (s.sba == id && s.gin == 0 && s.fl == 1) s.rew[i] -= 1.f;
             s.rew[i] += s.attr[i][8];
@@ -977,7 +978,7 @@ template <int N>
 BB_HD void sys_reward(World<N> &s)
 {
 #pragma unroll
-    for (int i = 0; i < N; i++) sys_reward_agent(s, i);
+    for (int i = 0; i < N; i++) sys_reward_agent(s, i, AGENT0_ID + i);
 }
 
 // ------------------------------------------------------------------ observations
@@ -1117,7 +1118,7 @@ BB_HD bool canonical_slots(const World<N> &s, int a)
 }
 
 template <int N>
-BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row)
+BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
 {
     RowSink o;
     o.row = row; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
@@ -1129,7 +1130,7 @@ BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row)
         if (j == a) continue;
         obs_agent_block(s, o, j, p, s.team[j] == s.team[a] ? att : dfn);
     }
-    const int32_t ib = inbounder_id(s);
+    // one-hot vectors over agents in creation order (absolute ids)
 #pragma unroll
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
 #pragma unroll
@@ -1138,7 +1139,7 @@ BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row)
 }
 
 template <int N>
-BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row)
+BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
 {
     SlowRowSink o;
     o.row = row; o.idx = 0;
@@ -1157,7 +1158,6 @@ BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row)
     }
     for (int k = mates; k < max_mates; k++) for (int z = 0; z < 37; z++) o.put(0.f);
     for (int k = opps; k < max_opps; k++) for (int z = 0; z < 37; z++) o.put(0.f);
-    const int32_t ib = inbounder_id(s);
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
     for (; o.idx < obs_width(N); ) o.put(0.f);
@@ -1166,11 +1166,12 @@ BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row)
 template <int N>
 BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
 {
+    const int32_t ib = inbounder_id(s);
 #pragma unroll
     for (int a = 0; a < N; a++) {
         float *row = c.p->c.obs + (c.w * N + a) * (int64_t)obs_width(N);
-        if (canonical_slots(s, a)) fill_obs_fast(s, c, a, row);
-        else fill_obs_slow(s, c, a, row);
+        if (canonical_slots(s, a)) fill_obs_fast(s, c, a, row, ib);
+        else fill_obs_slow(s, c, a, row, ib);
     }
 }
 
@@ -1212,6 +1213,62 @@ BB_HD void step_world(World<N> &s, Ctx &c)
     step_world_pre_obs(s, c);                      // 1-17
     sys_fill_obs(s, c);                            // 18
     sys_reward(s);                                 // 19
+}
+
+// ------------------------------------------------------------------ agent views
+// Copy of `s` with agent k in slot 0 and the other agents after it in
+// creation order (k runtime, every array index compile-time: register
+// selects, no scratch).  Systems that read "self" and "the others in
+// creation order" give identical results on the view's slot 0.
+template <class T, int N>
+BB_HD T pick(const T (&a)[N], int idx)
+{
+    T r = a[0];
+#pragma unroll
+    for (int i = 1; i < N; i++) r = (idx == i) ? a[i] : r;
+    return r;
+}
+
+template <int N>
+BB_HD int view_source(int slot, int k)  // absolute agent held by view slot
+{
+    return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
+}
+
+template <int N>
+BB_HD void agent_view(const World<N> &s, World<N> &v, int k)
+{
+    v = s;
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        const int src = view_source<N>(j, k);
+#define BB_V(f) v.f[j] = pick(s.f, src);
+        BB_V(rst) BB_V(cd) BB_V(px) BB_V(py) BB_V(pz) BB_V(rew) BB_V(done) BB_V(step)
+        BB_V(has) BB_V(bid) BB_V(pw) BB_V(qw) BB_V(qx) BB_V(qy) BB_V(qz) BB_V(inb) BB_V(allow)
+        BB_V(team) BB_V(dhoop) BB_V(vx) BB_V(vy) BB_V(vz)
+#undef BB_V
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            int32_t col[N];
+#pragma unroll
+            for (int i = 0; i < N; i++) col[i] = s.act[i][q];
+            v.act[j][q] = pick(col, src);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            int32_t col[N];
+#pragma unroll
+            for (int i = 0; i < N; i++) col[i] = s.msk[i][q];
+            v.msk[j][q] = pick(col, src);
+        }
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            float col[N];
+#pragma unroll
+            for (int i = 0; i < N; i++) col[i] = s.attr[i][q];
+            v.attr[j][q] = pick(col, src);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ load/store
@@ -1302,10 +1359,9 @@ BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w)
 // Per-agent columns of agent i (row w*N + i of every [W][N][...] column).
 // Team changes only inside generate/reset, which write it directly.
 template <int N>
-BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t w, int i)
+BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int i)
 {
     const Columns &c = p.c;
-    const int64_t r = w * N + i;
     uint32_t a[6], m[4], pos[3], ps[3], q[4], v[3], ib[2], at[10];
 #pragma unroll
     for (int k = 0; k < 6; k++) a[k] = (uint32_t)s.act[i][k];
@@ -1338,7 +1394,7 @@ BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
 {
     store_world_shared(s, p, w);
 #pragma unroll
-    for (int i = 0; i < N; i++) store_world_agent(s, p, w, i);
+    for (int i = 0; i < N; i++) store_world_agent(s, p, w * N + i, i);
 }
 
 // Constant columns written once at construction: entity ids, hoop positions.
