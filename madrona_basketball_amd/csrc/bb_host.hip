@@ -551,6 +551,9 @@ int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
 int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t write_q, void *stream,
                  float *avg_ms)
 {
+    // mode = 5 + 8 * skip-mask: MODE_SKIP with Params::diag_skip = mask
+    uint32_t skip = 0;
+    if (mode >= 5 && mode < 100) { skip = (uint32_t)(mode - 5) / 8u; mode = 5; }
     if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || iters < 1 || !avg_ms) return fail(BB_ERR_INVALID_ARG, "bb_diag_time");
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;
@@ -564,9 +567,11 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
+    bb::Params pp = s->p;
+    pp.diag_skip = skip;
     auto once = [&]() -> hipError_t {
         if (mode == 100) return bb::launch_stream_probe(src, dst, W, read_q, write_q, st);
-        return bb::launch_step(s->n, s->p, st, mode);
+        return bb::launch_step(s->n, pp, st, mode);
     };
     hipError_t e = once();  // warm
     if (e == hipSuccess) {

@@ -41,9 +41,12 @@ struct ObsTile {
 // all hold the full world state and run systems 1-17 identically, but each
 // computes and stores only its own agent's observation row, reward and
 // per-agent columns; the world-level columns are stored by the agent-0 lane.
+#ifndef BB_AGENT_LANES
+#define BB_AGENT_LANES 0  // measured slower at N=2 (duplicated systems, LDS-limited residency)
+#endif
 template <int N>
 struct Lanes {
-    static constexpr int LPW = (N == 2 || N == 4) ? N : 1;
+    static constexpr int LPW = (BB_AGENT_LANES && (N == 2 || N == 4)) ? N : 1;
     static constexpr int WPB = WAVE / LPW;  // worlds per 64-lane workgroup
 };
 
@@ -83,7 +86,8 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
     Ctx c = make_ctx(p, w, k == 0);
     if (active) {
         load_world(s, p, w);
-        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
+        if constexpr (MODE == MODE_SKIP) step_world_pre_obs_diag(s, c, p.diag_skip);
+        else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
     // ---------------------------------------------------------- observations
     // view of the world with this lane's agent in slot 0 (LPW == N)
@@ -156,6 +160,7 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s)
     case MODE_IO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO_OBS>), grid, block, 0, s, p); break;
     case MODE_DIRECT_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_DIRECT_OBS>), grid, block, 0, s, p); break;
     case MODE_NO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_NO_OBS>), grid, block, 0, s, p); break;
+    case MODE_SKIP: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_SKIP>), grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -14,6 +14,7 @@ enum StepMode : int {
     MODE_IO_OBS = 2,      // load + observation rows + store, no systems
     MODE_DIRECT_OBS = 3,  // 19 systems, observation rows stored lane-strided (v1)
     MODE_NO_OBS = 4,      // systems 1-17 and 19, no observation rows
+    MODE_SKIP = 5,        // full, minus the systems whose bit is set in Params::diag_skip
 };
 
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s);

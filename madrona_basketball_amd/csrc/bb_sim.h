@@ -191,6 +191,7 @@ struct Params {
     Q4 start_q[2];               // angleAxis(-pi/2, z), angleAxis(+pi/2, z)     gen.cpp:196
     float rot_thresh;            // (float)acos(c) > pi/8  <=>  c < rot_thresh   game.cpp:746-747
     int32_t rot_exact;           // 1: threshold not verified, evaluate acos
+    uint32_t diag_skip;          // diagnostics only (MODE_SKIP): systems to leave out
 };
 
 BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
@@ -1205,6 +1206,33 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c)
     sys_points_worth(s, c);                        // 15
     sys_collisions(s);                             // 16
     sys_defense(s, c);                             // 17
+}
+
+// Diagnostic copy of systems 1-17 that leaves out the systems whose bit
+// (1 << system number) is set -- timing attribution only, not the game.
+template <int N>
+BB_HD void step_world_pre_obs_diag(World<N> &s, Ctx &c, uint32_t skip)
+{
+    const uint32_t flags = c.p->flags;
+#define BB_RUN(bit, stmt) if (!(skip & (1u << (bit)))) { stmt; }
+    BB_RUN(1, sys_tick(s))
+    BB_RUN(2, sys_action_mask(s, flags))
+    BB_RUN(3, sys_move_agents(s, c))
+    BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, i))
+    BB_RUN(5, for (int i = 0; i < N; i++) sys_pass(s, i))
+    BB_RUN(6, for (int i = 0; i < N; i++) sys_shoot(s, c, i))
+    BB_RUN(7, sys_move_ball(s, c))
+    BB_RUN(8, sys_shot_percentage(s, c))
+    BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))
+    BB_RUN(10, sys_out_of_bounds(s, c))
+    BB_RUN(11, sys_last_touch(s))
+    BB_RUN(12, sys_clock(s))
+    BB_RUN(13, sys_inbound_violation(s, c))
+    BB_RUN(14, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })
+    BB_RUN(15, sys_points_worth(s, c))
+    BB_RUN(16, sys_collisions(s))
+    BB_RUN(17, sys_defense(s, c))
+#undef BB_RUN
 }
 
 template <int N>
