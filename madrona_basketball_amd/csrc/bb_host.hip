@@ -551,9 +551,8 @@ int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
 int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t write_q, void *stream,
                  float *avg_ms)
 {
-    // mode = 5 + 8 * skip-mask: MODE_SKIP with Params::diag_skip = mask
-    uint32_t skip = 0;
-    if (mode >= 5 && mode < 100) { skip = (uint32_t)(mode - 5) / 8u; mode = 5; }
+    // MODE_SKIP (5): read_q carries the skip mask (Params::diag_skip)
+    const uint32_t skip = (mode == 5) ? (uint32_t)read_q : 0u;
     if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || iters < 1 || !avg_ms) return fail(BB_ERR_INVALID_ARG, "bb_diag_time");
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;

@@ -26,21 +26,21 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     snap = sim.snapshot()
 
-    def t(mode):
+    def t(mode, skip=0):
         v = []
         for _ in range(a.rounds):
             sim.restore(snap)
             ms = ctypes.c_float()
-            assert L.bb_diag_time(sim._h, mode, a.iters, 0, 0, st, ctypes.byref(ms)) == 0, L.bb_last_error()
+            assert L.bb_diag_time(sim._h, mode, a.iters, skip, 0, st, ctypes.byref(ms)) == 0, L.bb_last_error()
             v.append(ms.value * 1e3)
         return statistics.median(v)
     base = t(5)  # MODE_SKIP with empty mask == full
     full = t(0)
     print(f"full {full:.2f} us, skip-mode baseline {base:.2f} us, no-obs {t(4):.2f}, io {t(1):.2f}")
     for b, n in NAMES.items():
-        x = t(5 + 8 * (1 << b))
+        x = t(5, 1 << b)
         print(f"  without {n:12s} {x:8.2f} us   saves {base - x:6.2f} us")
-    allsys = t(5 + 8 * sum(1 << b for b in NAMES))
+    allsys = t(5, sum(1 << b for b in NAMES))
     print(f"  without all systems {allsys:.2f} us")
 
 
