@@ -99,7 +99,13 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
             agent_view(s, v, k);
         }
     }
-    if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
+    if constexpr (LPW != N && (MODE == MODE_IO || MODE == MODE_NO_OBS)) {
+        if (active) {
+            if constexpr (MODE == MODE_NO_OBS) sys_reward(s);
+            store_world(s, p, w);
+        }
+        return;
+    } else if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
     } else if constexpr (LPW == N) {
         float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
         if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
@@ -115,19 +121,39 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
             // lane = (w - w0) * N + k: the wave's rows are consecutive in memory
             flush_tile<N>(tile, p.c.obs, w0 * N, 1, __ballot(fast), lane);
         }
-    } else if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
-        if (active) sys_fill_obs(s, c);
     } else {
-        const int32_t ib1 = active ? inbounder_id(s) : -1;
-#pragma unroll
-        for (int a = 0; a < N; a++) {
-            const bool fast = active && canonical_slots(s, a);
-            if (fast) fill_obs_fast(s, c, a, tile + lane * T::RS, ib1);
-            else if (active) fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW, ib1);
-            __syncthreads();
-            flush_tile<N>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
-            __syncthreads();
+        // one lane per world: reward + state columns first, so their stores
+        // drain while the observation rows are built
+        if (active) {
+            if constexpr (MODE != MODE_IO_OBS) sys_reward(s);
+            store_world(s, p, w);
         }
+        if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
+            if (active) sys_fill_obs(s, c);
+        } else {
+            const int32_t ib1 = active ? inbounder_id(s) : -1;
+            const bool share = active && obs_sharable(s);
+            SharedObs<N> sh;
+            if (share) shared_obs_prepare(s, c, sh);
+#pragma unroll
+            for (int a = 0; a < N; a++) {
+                float *trow = tile + lane * T::RS;
+                const bool fast = active && (share || canonical_slots(s, a));
+                if (share) {
+                    RowSink o;
+                    o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                    emit_row_shared(s, c, sh, a, o, ib1);
+                } else if (fast) {
+                    fill_obs_fast(s, c, a, trow, ib1);
+                } else if (active) {
+                    fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW, ib1);
+                }
+                __syncthreads();
+                flush_tile<N>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
+                __syncthreads();
+            }
+        }
+        return;
     }
     // ---------------------------------------------------------- reward + store
     if (!active) return;
@@ -135,9 +161,6 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
         store_world_agent(v, p, w * N + k, 0);
         if (k == 0) store_world_shared(s, p, w);
-    } else {
-        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);
-        store_world(s, p, w);
     }
 }
 

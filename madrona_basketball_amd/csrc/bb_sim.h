@@ -1017,13 +1017,16 @@ struct SlowRowSink {
     BB_HD void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
 };
 
+// The 31 values of an agent block that depend only on agent j and the hoop it
+// is measured against (game.cpp:1293-1322 for self, :1343-1372 / :1384-1421
+// for teammates / opponents): orientation, forward, velocity direction,
+// speed, facing dot, acceleration factor, hoop direction + distance, ball
+// direction + distance, inbounding, cooldown, 6 attributes, pointsWorth,
+// hasBall.
 template <int N, class Sink>
-BB_HD void obs_agent_block(const World<N> &s, Sink &o, int j, F3 self_pos, F3 hoop)
+BB_HD void emit_intrinsic(const World<N> &s, Sink &o, int j, F3 hoop)
 {
-    const F3 pj = s.pos(j), to = pj - self_pos;
-    o.put3(pj);
-    o.put3(len2(to) > 1e-6f ? norm(to) : f3(0.f, 0.f, 0.f));
-    o.put(len(to));
+    const F3 pj = s.pos(j);
     const Q4 qj = s.q(j);
     o.put4(qj);
     const F3 fw = forward(qj);
@@ -1050,9 +1053,37 @@ BB_HD void obs_agent_block(const World<N> &s, Sink &o, int j, F3 self_pos, F3 ho
     o.put((float)s.pw[j]);
     o.put((float)s.has[j]);
 }
+constexpr int INTRINSIC = 31;
+
+// A fixed-size buffer sink (compile-time indices fold it into registers).
+template <int LEN>
+struct ArraySink {
+    float v[LEN];
+    int idx;
+    BB_HD void put(float x) { v[idx++] = x; }
+    BB_HD void put3(F3 a) { put(a.x); put(a.y); put(a.z); }
+    BB_HD void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+};
 
 template <int N, class Sink>
-BB_HD void obs_header(const World<N> &s, const Ctx &c, Sink &o, int a, F3 *att, F3 *dfn)
+BB_HD void obs_agent_block(const World<N> &s, Sink &o, int j, F3 self_pos, F3 hoop)
+{
+    const F3 pj = s.pos(j), to = pj - self_pos;
+    o.put3(pj);
+    o.put3(len2(to) > 1e-6f ? norm(to) : f3(0.f, 0.f, 0.f));
+    o.put(len(to));
+    emit_intrinsic(s, o, j, hoop);
+}
+
+template <int N>
+BB_HD F3 attacking_hoop(const World<N> &s, const Ctx &c, int a)  // game.cpp:1284
+{
+    return (HOOP0_ID != s.dhoop[a]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+}
+
+// Game context + egocentric score + ball + hoops (obs 0-22, game.cpp:1256-1287)
+template <int N, class Sink>
+BB_HD void obs_context(const World<N> &s, const Ctx &c, Sink &o, int a, F3 *att, F3 *dfn)
 {
     o.put(s.g_clock); o.put(s.g_shot); o.put(s.g_period);
     o.put((float)s.g_inb); o.put(s.g_inbclk);
@@ -1060,39 +1091,20 @@ BB_HD void obs_header(const World<N> &s, const Ctx &c, Sink &o, int a, F3 *att, 
     o.put(s.team[a] == 0 ? s.g_s1 : s.g_s0);
     o.put3(s.bpos()); o.put3(s.bvel());
     o.put((float)s.grab); o.put((float)s.fl); o.put((float)s.spv); o.put((float)s.ltt);
-    *att = (HOOP0_ID != s.dhoop[a]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+    *att = attacking_hoop(s, c, a);
     *dfn = (HOOP0_ID == s.dhoop[a]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
     o.put3(*att); o.put3(*dfn);
-    // self block (23..60): position, 4 zeros, then the shared agent fields
-    const F3 p = s.pos(a);
-    o.put3(p);
+}
+
+template <int N, class Sink>
+BB_HD void obs_header(const World<N> &s, const Ctx &c, Sink &o, int a, F3 *att, F3 *dfn)
+{
+    obs_context(s, c, o, a, att, dfn);
+    // self block (23..60): position, 4 zeros, then the intrinsic values
+    o.put3(s.pos(a));
     o.put3(f3(0.f, 0.f, 0.f));
     o.put(0.f);
-    const Q4 q = s.q(a);
-    o.put4(q);
-    const F3 fw = forward(q);
-    o.put3(fw);
-    const F3 v = s.vel(a);
-    const bool moving = len2(v) > 1e-6f;
-    o.put3(moving ? norm(v) : f3(0.f, 0.f, 0.f));
-    o.put(len(v));
-    const float d = moving ? dot(norm(v), fw) : 0.f;
-    o.put(d);
-    o.put(d <= 0.8f ? 0.1f : 1.f);
-    const F3 th = *att - p;
-    const float dh = len(th);
-    o.put3(dh > 1e-6f ? norm(th) : f3(0.f, 0.f, 0.f));
-    o.put(dh);
-    const F3 tb = s.bpos() - p;
-    const float db = len(tb);
-    o.put3(db > 1e-6f ? norm(tb) : f3(0.f, 0.f, 0.f));
-    o.put(db);
-    o.put((float)s.inb[a]);
-    o.put(s.cd[a]);
-    o.put(s.attr[a][0]); o.put(s.attr[a][1]); o.put(s.attr[a][2]);
-    o.put(s.attr[a][3]); o.put(s.attr[a][4]); o.put(s.attr[a][8]);
-    o.put((float)s.pw[a]);
-    o.put((float)s.has[a]);
+    emit_intrinsic(s, o, a, *att);
 }
 
 template <int N>
@@ -1139,6 +1151,84 @@ BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row, int
     o.finish();
 }
 
+// Observation rows of every agent of a world with each agent's intrinsic
+// block computed once (canonical layouts in which the hoop an observer
+// measures agent j against is j's own attacking hoop -- always the case for
+// the generated teams): bit-identical to fill_obs_fast per agent.
+template <int N>
+BB_HD bool obs_sharable(const World<N> &s)
+{
+#pragma unroll
+    for (int a = 0; a < N; a++) {
+        if (!canonical_slots(s, a)) return false;
+        const bool att0_a = HOOP0_ID != s.dhoop[a];
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            if (j == a) continue;
+            // observer a measures j against a's attacking hoop if j is a
+            // teammate, else a's defending hoop; j's own attacking hoop:
+            const bool chosen0 = (s.team[j] == s.team[a]) ? att0_a : (HOOP0_ID == s.dhoop[a]);
+            if (chosen0 != (HOOP0_ID != s.dhoop[j])) return false;
+        }
+    }
+    return true;
+}
+
+template <int N>
+struct SharedObs {
+    ArraySink<INTRINSIC> intr[N];
+    F3 rdir[N][N];   // direction from a to j (0 vector below the 1e-6 threshold)
+    float rlen[N][N];
+};
+
+template <int N>
+BB_HD void shared_obs_prepare(const World<N> &s, const Ctx &c, SharedObs<N> &sh)
+{
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        sh.intr[j].idx = 0;
+        emit_intrinsic(s, sh.intr[j], j, attacking_hoop(s, c, j));
+    }
+#pragma unroll
+    for (int a = 0; a < N; a++)
+#pragma unroll
+        for (int j = a + 1; j < N; j++) {
+            const F3 to = s.pos(j) - s.pos(a), back = s.pos(a) - s.pos(j);
+            const float l2 = len2(to);                        // == len2(back) exactly
+            const bool nz = l2 > 1e-6f;
+            const float r = 1.0f / bbm::sqrtf_(l2);           // the factor norm() applies
+            sh.rdir[a][j] = nz ? to * r : f3(0.f, 0.f, 0.f);
+            sh.rdir[j][a] = nz ? back * r : f3(0.f, 0.f, 0.f);  // not -(to * r): +0 stays +0
+            sh.rlen[a][j] = sh.rlen[j][a] = bbm::sqrtf_(l2);
+        }
+}
+
+template <int N, class Sink>
+BB_HD void emit_row_shared(const World<N> &s, const Ctx &c, const SharedObs<N> &sh, int a, Sink &o, int32_t ib)
+{
+    F3 att, dfn;
+    obs_context(s, c, o, a, &att, &dfn);
+    o.put3(s.pos(a));
+    o.put3(f3(0.f, 0.f, 0.f));
+    o.put(0.f);
+#pragma unroll
+    for (int q = 0; q < INTRINSIC; q++) o.put(sh.intr[a].v[q]);
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+        if (j == a) continue;
+        o.put3(s.pos(j));
+        o.put3(sh.rdir[a][j]);
+        o.put(sh.rlen[a][j]);
+#pragma unroll
+        for (int q = 0; q < INTRINSIC; q++) o.put(sh.intr[j].v[q]);
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
+    o.finish();
+}
+
 template <int N>
 BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
 {
@@ -1168,6 +1258,18 @@ template <int N>
 BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
 {
     const int32_t ib = inbounder_id(s);
+    if (obs_sharable(s)) {
+        SharedObs<N> sh;
+        shared_obs_prepare(s, c, sh);
+#pragma unroll
+        for (int a = 0; a < N; a++) {
+            RowSink o;
+            o.row = c.p->c.obs + (c.w * N + a) * (int64_t)obs_width(N);
+            o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+            emit_row_shared(s, c, sh, a, o, ib);
+        }
+        return;
+    }
 #pragma unroll
     for (int a = 0; a < N; a++) {
         float *row = c.p->c.obs + (c.w * N + a) * (int64_t)obs_width(N);
@@ -1239,8 +1341,8 @@ template <int N>
 BB_HD void step_world(World<N> &s, Ctx &c)
 {
     step_world_pre_obs(s, c);                      // 1-17
+    sys_reward(s);                                 // 19 (reads nothing fillObservations writes)
     sys_fill_obs(s, c);                            // 18
-    sys_reward(s);                                 // 19
 }
 
 // ------------------------------------------------------------------ agent views
