@@ -47,12 +47,15 @@ def cpu_baseline(num_agents: int, seconds: float):
 
 
 def load_traffic(workload_key: str):
+    """HBM bytes per step-kernel launch from the committed PMC passes
+    (tools/traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get(workload_key)
-    except (OSError, ValueError):
+        e = d.get(workload_key)
+        return None if e is None else e["bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
         return None
 
 

@@ -59,6 +59,7 @@ for s in $STEPS; do
             --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline ) || exit $?
         ( cd /tmp && export TMPDIR=/tmp && run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run \
             --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline ) || exit $?
+        python3 tools/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" W65536_N2 --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
         ;;
     *) echo "unknown step $s" ;;
     esac
