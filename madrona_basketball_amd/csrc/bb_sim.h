@@ -144,6 +144,20 @@ BB_HD int32_t shot_point_value(F3 p, F3 hz)
     return d >= ARC ? 3 : 2;
 }
 
+// Value of f(j) for j == i, built from selects (i may be a runtime value --
+// e.g. the lane's agent -- while every array index inside f stays constant).
+template <int N, class F>
+BB_HD auto pick_by(int i, F f) -> decltype(f(0))
+{
+    auto r = f(0);
+#pragma unroll
+    for (int j = 1; j < N; j++) {
+        auto x = f(j);
+        r = (i == j) ? x : r;
+    }
+    return r;
+}
+
 // ------------------------------------------------------------------ layout
 // Column pointers.  Exported columns keep the reference byte layouts;
 // *_u views reinterpret mixed int/float structs (GameState, Team, Stats).
@@ -566,43 +580,84 @@ BB_HD void sys_action_mask(World<N> &s, uint32_t flags)  // game.cpp:489-533
     }
 }
 
+// ---- moveAgentSystem (game.cpp:410-486), one agent ---------------------
+struct MoveIn {
+    int32_t rotate, move, angle, can_move, has;
+    Q4 q;
+    F3 vel;
+    float px, py, max_speed, quickness;
+};
+struct MoveOut {
+    Q4 q;
+    F3 vel;
+    float px, py;
+};
+
 template <int N>
-BB_HD void sys_move_agents(World<N> &s, const Ctx &c)  // game.cpp:410-486
+BB_HD MoveIn gather_move(const World<N> &s, int i)
+{
+    MoveIn m;
+    m.rotate = pick_by<N>(i, [&](int j) { return s.act[j][2]; });
+    m.move = pick_by<N>(i, [&](int j) { return s.act[j][0]; });
+    m.angle = pick_by<N>(i, [&](int j) { return s.act[j][1]; });
+    m.can_move = pick_by<N>(i, [&](int j) { return s.msk[j][0]; });
+    m.has = pick_by<N>(i, [&](int j) { return s.has[j]; });
+    m.q = pick_by<N>(i, [&](int j) { return s.q(j); });
+    m.vel = pick_by<N>(i, [&](int j) { return s.vel(j); });
+    m.px = pick_by<N>(i, [&](int j) { return s.px[j]; });
+    m.py = pick_by<N>(i, [&](int j) { return s.py[j]; });
+    m.max_speed = pick_by<N>(i, [&](int j) { return s.attr[j][0]; });
+    m.quickness = pick_by<N>(i, [&](int j) { return s.attr[j][1]; });
+    return m;
+}
+
+BB_HD MoveOut move_one(const MoveIn &in, const Params &p)
+{
+    MoveOut o;
+    o.q = in.q;
+    if (in.rotate != 0) o.q = qmul(in.rotate == 1 ? p.turn_q[0] : p.turn_q[1], in.q);
+    o.vel = in.vel; o.px = in.px; o.py = in.py;
+    if (in.can_move == 0) return o;
+    const int32_t m = in.angle;
+    float sn = p.mv_sin[0], cs = p.mv_cos[0];
+    if ((uint32_t)m < 8u) {
+#pragma unroll
+        for (int k = 1; k < 8; k++)
+            if (m == k) { sn = p.mv_sin[k]; cs = p.mv_cos[k]; }
+    } else {
+        bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
+    }
+    F3 dv = (f3(sn, -cs, 0.f) * in.quickness) * (float)in.move;
+    float maxs = in.max_speed;
+    const F3 fw = forward(o.q);
+    F3 v = in.vel;
+    float d = 0.f;
+    if (len2(v) > 1e-6f) d = dot(norm(v), fw);
+    if (d < -0.1f) { maxs *= .1f; dv = dv * .1f; }
+    else if (d <= 0.8f) { maxs *= .7f; dv = dv * .1f; }
+    v = v + dv;
+    if (in.has == 1) maxs *= BALL_SLOW;
+    if (len(v) > maxs) v = v * (maxs / len(v));
+    const float dx = v.x * TS, dy = v.y * TS;
+    // the binding's grid is all-empty (src/bindings.cpp:7-11): the wall
+    // lookup of game.cpp:472-484 always accepts the move.
+    o.px = clampf(in.px + dx, 0.f, p.width);
+    o.py = clampf(in.py + dy, 0.f, p.height);
+    o.vel = v * .95f;
+    return o;
+}
+
+template <int N>
+BB_HD void apply_move(World<N> &s, int j, const MoveOut &o)
+{
+    s.set_q(j, o.q); s.set_vel(j, o.vel); s.px[j] = o.px; s.py[j] = o.py;
+}
+
+template <int N>
+BB_HD void sys_move_agents(World<N> &s, const Ctx &c)
 {
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        if (s.act[i][2] != 0) {
-            const Q4 turn = s.act[i][2] == 1 ? c.p->turn_q[0] : c.p->turn_q[1];
-            s.set_q(i, qmul(turn, s.q(i)));
-        }
-        if (s.msk[i][0] == 0) continue;
-        const int32_t m = s.act[i][1];
-        float sn = c.p->mv_sin[0], cs = c.p->mv_cos[0];
-        if ((uint32_t)m < 8u) {
-#pragma unroll
-            for (int k = 1; k < 8; k++)
-                if (m == k) { sn = c.p->mv_sin[k]; cs = c.p->mv_cos[k]; }
-        } else {
-            bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
-        }
-        F3 dv = (f3(sn, -cs, 0.f) * s.attr[i][1]) * (float)s.act[i][0];
-        float maxs = s.attr[i][0];
-        const F3 fw = forward(s.q(i));
-        F3 v = s.vel(i);
-        float d = 0.f;
-        if (len2(v) > 1e-6f) d = dot(norm(v), fw);
-        if (d < -0.1f) { maxs *= .1f; dv = dv * .1f; }
-        else if (d <= 0.8f) { maxs *= .7f; dv = dv * .1f; }
-        v = v + dv;
-        if (s.has[i] == 1) maxs *= BALL_SLOW;
-        if (len(v) > maxs) v = v * (maxs / len(v));
-        const float dx = v.x * TS, dy = v.y * TS;
-        // the binding's grid is all-empty (src/bindings.cpp:7-11): the wall
-        // lookup of game.cpp:472-484 always accepts the move.
-        s.px[i] = clampf(s.px[i] + dx, 0.f, c.p->width);
-        s.py[i] = clampf(s.py[i] + dy, 0.f, c.p->height);
-        s.set_vel(i, v * .95f);
-    }
+    for (int i = 0; i < N; i++) apply_move(s, i, move_one(gather_move(s, i), *c.p));
 }
 
 template <int N>
@@ -712,30 +767,41 @@ BB_HD void sys_move_ball(World<N> &s, const Ctx &c)  // game.cpp:82-125
     s.bx = nx; s.by = ny; s.bz = nz;  // empty grid: never a wall (game.cpp:118-124)
 }
 
+// ---- updateCurrentShotPercentage (game.cpp:758-809), one agent ---------
 template <int N>
-BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c)  // game.cpp:758-809
+BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
 {
+    const int32_t has = pick_by<N>(i, [&](int j) { return s.has[j]; });
+    if (has == 0) return 0.f;
+    const F3 p = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const int32_t team = pick_by<N>(i, [&](int j) { return s.team[j]; });
+    const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
+    const F3 hoop = (HOOP0_ID != dhoop) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
+    const float dh = len(hoop - p);
+    float nd = __builtin_inff();
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        if (s.has[i] == 0) { s.attr[i][8] = 0.f; continue; }
-        const F3 p = s.pos(i);
-        const F3 hoop = (HOOP0_ID != s.dhoop[i]) ? hoop_pos<N>(c, 0) : hoop_pos<N>(c, 1);
-        const float dh = len(hoop - p);
-        float nd = __builtin_inff();
-#pragma unroll
-        for (int j = 0; j < N; j++) {
-            if (s.team[j] != s.team[i]) {
-                const float dd = len(p - s.pos(j));
-                if (dd < nd) nd = dd;
-            }
+    for (int j = 0; j < N; j++) {
+        if (s.team[j] != team) {
+            const float dd = len(p - s.pos(j));
+            if (dd < nd) nd = dd;
         }
-        const float ds = DIST_DEV * dh;
-        const float fs = DEF_DEV / nd + .0001f;
-        const float vs = VEL_DEV * len(s.vel(i));
-        const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
-        const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
-        s.attr[i][8] = (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)));
     }
+    const float ds = DIST_DEV * dh;
+    const float fs = DEF_DEV / nd + .0001f;
+    const float vs = VEL_DEV * len(pick_by<N>(i, [&](int j) { return s.vel(j); }));
+    const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
+    const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
+    return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)));
+}
+
+template <int N>
+BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c)
+{
+    float v[N];
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] = shot_pct_one(s, c, i);  // reads nothing it writes
+#pragma unroll
+    for (int i = 0; i < N; i++) s.attr[i][8] = v[i];
 }
 
 template <int N>
@@ -834,16 +900,23 @@ BB_HD void sys_inbound_violation(World<N> &s, Ctx &c)  // game.cpp:1116-1157
     }
 }
 
+// ---- updatePointsWorthSystem (game.cpp:129-161), one agent -------------
 template <int N>
-BB_HD void sys_points_worth(World<N> &s, const Ctx &c)  // game.cpp:129-161
+BB_HD int32_t points_worth_one(const World<N> &s, const Ctx &c, int i)
+{
+    // first hoop (creation order) that is not defended; both are never defended at once
+    const F3 p = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
+    if (HOOP0_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 0));
+    if (HOOP1_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 1));
+    return 2;
+}
+
+template <int N>
+BB_HD void sys_points_worth(World<N> &s, const Ctx &c)
 {
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        // first hoop (creation order) that is not defended; both are never defended at once
-        if (HOOP0_ID != s.dhoop[i]) s.pw[i] = shot_point_value(s.pos(i), hoop_pos<N>(c, 0));
-        else if (HOOP1_ID != s.dhoop[i]) s.pw[i] = shot_point_value(s.pos(i), hoop_pos<N>(c, 1));
-        else s.pw[i] = 2;
-    }
+    for (int i = 0; i < N; i++) s.pw[i] = points_worth_one(s, c, i);  // reads only pos/dhoop
 }
 
 struct Proj { float mn, mx; };
@@ -901,78 +974,115 @@ BB_HD void sys_collisions(World<N> &s)
         for (int b = a + 1; b < N; b++) collide_pair(s, a, b);
 }
 
+// ---- hardCodeDefenseSystem (game.cpp:651-755), one agent --------------
+struct DefOut {
+    int32_t act[4];  // move, moveAngle, rotate, grab
+    F3 target;       // Attributes.currentTargetPosition
+};
+
 template <int N>
-BB_HD void sys_defense(World<N> &s, const Ctx &c)  // game.cpp:651-755
+BB_HD DefOut defense_one(const World<N> &s, const Ctx &c, int i)
 {
+    DefOut o;
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        if (s.g_poss == (float)s.team[i]) { s.act[i][0] = 0; continue; }
-        s.act[i][3] = 1;
-        F3 guard = f3(0.f, 0.f, 0.f);
-        bool found = false;
+    for (int q = 0; q < 4; q++) o.act[q] = pick_by<N>(i, [&](int j) { return s.act[j][q]; });
+    o.target = pick_by<N>(i, [&](int j) { return s.target(j); });
+    const int32_t team = pick_by<N>(i, [&](int j) { return s.team[j]; });
+    if (s.g_poss == (float)team) { o.act[0] = 0; return o; }
+    o.act[3] = 1;
+    const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
+    F3 guard = f3(0.f, 0.f, 0.f);
+    bool found = false;
 #pragma unroll
-        for (int j = 0; j < N; j++) {
-            if (s.has[j] == 1 && !found) {
+    for (int j = 0; j < N; j++) {
+        if (s.has[j] == 1 && !found) {
 #pragma unroll
-                for (int h = 0; h < 2; h++) {
-                    if (s.dhoop[i] == (h == 0 ? HOOP0_ID : HOOP1_ID)) {
-                        const F3 hd = hoop_pos<N>(c, h) - s.pos(j);
-                        guard = (len2(hd) > 1e-6f) ? s.pos(j) + norm(hd) * GUARD : s.pos(j);
-                        found = true;
-                    }
+            for (int h = 0; h < 2; h++) {
+                if (dhoop == (h == 0 ? HOOP0_ID : HOOP1_ID)) {
+                    const F3 hd = hoop_pos<N>(c, h) - s.pos(j);
+                    guard = (len2(hd) > 1e-6f) ? s.pos(j) + norm(hd) * GUARD : s.pos(j);
+                    found = true;
                 }
             }
         }
-        if (!found) { s.act[i][0] = 0; continue; }
-        const F3 cur = s.target(i);
-        s.set_target(i, cur + (guard - cur) * (s.attr[i][4] * TS));
-        const F3 mv = s.target(i) - s.pos(i);
-        if (len2(mv) < 0.01f) { s.act[i][0] = 0; continue; }
-        // argmax over the 8 move directions of game.cpp:713-722 (first max wins)
-        const F3 desired = norm(mv);
-        const float diag = 1.0f / bbm::sqrtf_(2.f);
-        const float dots[8] = {
-            dot(desired, f3(0.f * 1.f, -1.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, -1.f * diag, 0.f * diag)),
-            dot(desired, f3(1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, 1.f * diag, 0.f * diag)),
-            dot(desired, f3(0.f * 1.f, 1.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, 1.f * diag, 0.f * diag)),
-            dot(desired, f3(-1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, -1.f * diag, 0.f * diag))};
-        float maxd = -2.f;
-        int32_t best = 0;
-#pragma unroll
-        for (int k = 0; k < 8; k++)
-            if (dots[k] > maxd) { maxd = dots[k]; best = k; }
-        s.act[i][0] = 1;
-        s.act[i][1] = best;
-        const F3 fw = forward(s.q(i));
-        const float cosang = clampf(dot(fw, norm(mv)), -1.f, 1.f);
-        const bool turn = c.p->rot_exact ? ((float)bbm::acos_d((double)cosang) > PI_OVER_8)
-                                         : (cosang < c.p->rot_thresh);
-        if (turn) {
-            const float cr = fw.x * mv.y - fw.y * mv.x;
-            s.act[i][2] = cr < 0.f ? -1 : (cr > 0.f ? 1 : 0);
-        } else {
-            s.act[i][2] = 0;
-        }
     }
+    if (!found) { o.act[0] = 0; return o; }
+    const F3 cur = o.target;
+    const float react = pick_by<N>(i, [&](int j) { return s.attr[j][4]; });
+    o.target = cur + (guard - cur) * (react * TS);
+    const F3 mv = o.target - pick_by<N>(i, [&](int j) { return s.pos(j); });
+    if (len2(mv) < 0.01f) { o.act[0] = 0; return o; }
+    // argmax over the 8 move directions of game.cpp:713-722 (first max wins)
+    const F3 desired = norm(mv);
+    const float diag = 1.0f / bbm::sqrtf_(2.f);
+    const float dots[8] = {
+        dot(desired, f3(0.f * 1.f, -1.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, -1.f * diag, 0.f * diag)),
+        dot(desired, f3(1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(1.f * diag, 1.f * diag, 0.f * diag)),
+        dot(desired, f3(0.f * 1.f, 1.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, 1.f * diag, 0.f * diag)),
+        dot(desired, f3(-1.f * 1.f, 0.f * 1.f, 0.f)), dot(desired, f3(-1.f * diag, -1.f * diag, 0.f * diag))};
+    float maxd = -2.f;
+    int32_t best = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++)
+        if (dots[k] > maxd) { maxd = dots[k]; best = k; }
+    o.act[0] = 1;
+    o.act[1] = best;
+    const F3 fw = forward(pick_by<N>(i, [&](int j) { return s.q(j); }));
+    const float cosang = clampf(dot(fw, norm(mv)), -1.f, 1.f);
+    const bool turn = c.p->rot_exact ? ((float)bbm::acos_d((double)cosang) > PI_OVER_8)
+                                     : (cosang < c.p->rot_thresh);
+    if (turn) {
+        const float cr = fw.x * mv.y - fw.y * mv.x;
+        o.act[2] = cr < 0.f ? -1 : (cr > 0.f ? 1 : 0);
+    } else {
+        o.act[2] = 0;
+    }
+    return o;
 }
 
 template <int N>
-BB_HD void sys_reward_agent(World<N> &s, int i, int32_t id)  // game.cpp:811-870
+BB_HD void apply_defense(World<N> &s, int j, const DefOut &o)
 {
-    // `other` = the last agent (creation order) that is not self; with slot i
-    // the first of the others ascending (permuted view) this is slot N-1 too
-    const int other = (i == N - 1) ? N - 2 : N - 1;
-    const float dist = len(s.pos(other) - s.pos(i));
-    if ((float)s.team[i] == s.g_poss) {
+#pragma unroll
+    for (int q = 0; q < 4; q++) s.act[j][q] = o.act[q];
+    s.set_target(j, o.target);
+}
+
+template <int N>
+BB_HD void sys_defense(World<N> &s, const Ctx &c)
+{
+    // agent i reads only fields no other agent's defence writes
+#pragma unroll
+    for (int i = 0; i < N; i++) apply_defense(s, i, defense_one(s, c, i));
+}
+
+// ---- rewardSystem (game.cpp:811-870), one agent ------------------------
+template <int N>
+BB_HD float reward_one(const World<N> &s, int i, int32_t id)
+{
+    // `other` = the last agent (creation order) that is not self
+    const F3 p = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const F3 po = pick_by<N>(i, [&](int j) { return s.pos(j == N - 1 ? N - 2 : N - 1); });
+    const float dist = len(po - p);
+    float r = pick_by<N>(i, [&](int j) { return s.rew[j]; });
+    const int32_t team = pick_by<N>(i, [&](int j) { return s.team[j]; });
+    if ((float)team == s.g_poss) {
         if (s.g_clock > 5.f) {
-            if (s.sba == id && s.gin == 1) s.rew[i] += (float)s.spv;
-            else if (s.sba == id && s.gin == 0 && s.fl == 1) s.rew[i] -= 1.f;
-            s.rew[i] += s.attr[i][8];
+            if (s.sba == id && s.gin == 1) r += (float)s.spv;
+            else if (s.sba == id && s.gin == 0 && s.fl == 1) r -= 1.f;
+            r += pick_by<N>(i, [&](int j) { return s.attr[j][8]; });
         }
     } else {
-        s.rew[i] -= 1.f;
-        s.rew[i] = (float)((double)s.rew[i] + bbm::exp_d((double)(-0.4f * dist)));
+        r -= 1.f;
+        r = (float)((double)r + bbm::exp_d((double)(-0.4f * dist)));
     }
+    return r;
+}
+
+template <int N>
+BB_HD void sys_reward_agent(World<N> &s, int i, int32_t id)
+{
+    s.rew[i] = reward_one(s, i, id);
 }
 
 template <int N>
