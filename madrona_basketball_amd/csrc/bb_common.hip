@@ -86,6 +86,13 @@ hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode)
 #undef CALL
 }
 
+int step_grid_n(int n, int64_t num_worlds)
+{
+#define CALL(k) step_grid<k>(num_worlds)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
 hipError_t launch_init(int n, const Params &p, hipStream_t s)
 {
 #define CALL(k) launch_init_t<k>(p, s)

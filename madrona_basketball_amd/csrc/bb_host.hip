@@ -590,6 +590,28 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
     return BB_OK;
 }
 
+// Diagnostic (not in the public header): one MODE_TRACE launch; copies the
+// per-wave phase clocks (wall_clock64 ticks: start, systems done, state
+// stored, end) into out[waves][4].  *waves = number of waves of the launch.
+int bb_diag_trace(bb_sim *s, void *stream, uint64_t *out, int64_t max_waves, int64_t *waves)
+{
+    if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || !out || !waves) return fail(BB_ERR_INVALID_ARG, "bb_diag_trace");
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t nw = bb::step_grid_n(s->n, s->cfg.num_worlds);
+    *waves = nw;
+    if (nw > max_waves) return fail(BB_ERR_INVALID_ARG, "bb_diag_trace: out too small");
+    bb::Params pp = s->p;
+    if (hipMalloc(&pp.diag_ts, (size_t)nw * 4 * sizeof(uint64_t)) != hipSuccess) return fail(BB_ERR_OOM, "trace buffer");
+    hipError_t e = bb::launch_step(s->n, pp, st, bb::MODE_TRACE);  // warm
+    if (e == hipSuccess) e = bb::launch_step(s->n, pp, st, bb::MODE_TRACE);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, pp.diag_ts, (size_t)nw * 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(pp.diag_ts);
+    if (e != hipSuccess) return hip_fail(e, "diag trace");
+    return BB_OK;
+}
+
 int64_t bb_algorithmic_bytes_per_world(int32_t n)
 {
     // B(N) = N (268 + 4 obs_used(N)) + 152

@@ -5,15 +5,15 @@
 // agent (64/N worlds per wave), otherwise one lane per world.
 //   1. every lane loads its world's columns (16/8-byte vector loads where the
 //      per-world chunk allows) into a register-resident World<N>;
-//   2. systems 1-17 of src/game.cpp:1463-1526 run on registers (bb_sim.h),
-//      identically in the N lanes of a world;
-//   3. fillObservations (game.cpp:1175-1461): each lane writes its agent's
-//      row into an LDS tile (conflict-free ds_write_b128, row stride 4 mod 8
-//      dwords); the wave then stores the 64 rows -- consecutive in memory --
-//      as consecutive 16-byte pieces (whole 128-byte lines per instruction
-//      instead of 64 scattered ones);
-//   4. rewardSystem for the lane's agent, then the lane stores its agent's
-//      columns and the agent-0 lane the world columns.
+//   2. systems 1-17 of src/game.cpp:1463-1526 run on registers (bb_sim.h);
+//      with agent lanes the per-agent systems are split over the world's
+//      lanes and their results exchanged by DPP;
+//   3. rewardSystem, then the state columns are stored;
+//   4. fillObservations (game.cpp:1175-1461): rows go into an LDS tile
+//      (conflict-free ds_write_b128, row stride 4 mod 8 dwords); the wave
+//      then stores the 64 rows -- consecutive in memory -- as consecutive
+//      16-byte pieces (whole 128-byte lines per instruction instead of 64
+//      scattered ones).
 // Replaces the reference's 19 ParallelFor megakernel nodes + 3 sort nodes per
 // step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
@@ -37,12 +37,13 @@ struct ObsTile {
     static constexpr int FLOATS = STAGED ? WAVE * RS : 4;
 };
 
-// Lanes per world: with one lane per agent (N = 2, 4) the lanes of a world
-// all hold the full world state and run systems 1-17 identically, but each
-// computes and stores only its own agent's observation row, reward and
-// per-agent columns; the world-level columns are stored by the agent-0 lane.
+// Lanes per world.  With one lane per agent (N = 2, 4) each lane holds the
+// whole world and runs the world-level systems, but computes only its own
+// agent's share of the per-agent systems (move, shot percentage, points
+// worth, defence), reward, intrinsic observation block and observation row;
+// the other agents' results come from the neighbouring lanes by DPP.
 #ifndef BB_AGENT_LANES
-#define BB_AGENT_LANES 0  // measured slower at N=2 (duplicated systems, LDS-limited residency)
+#define BB_AGENT_LANES 1
 #endif
 template <int N>
 struct Lanes {
@@ -50,118 +51,294 @@ struct Lanes {
     static constexpr int WPB = WAVE / LPW;  // worlds per 64-lane workgroup
 };
 
-// Copy the wave's 64 staged rows (tile row r -> obs row base_row + r*stride)
-// as consecutive 16-byte pieces; rows whose bit is clear in `staged` were
-// written directly (generic layout) or belong to no world.
+// Row tile of the agent-lane kernel: the row is emitted in PH passes of QP
+// float4 pieces so the tile stays ~16 KB (>= 8 waves per CU).
 template <int N>
+struct PhasedTile {
+    static constexpr int QW = (obs_used(N) + 3) / 4;
+    static constexpr int PH = (QW + 14) / 15;
+    static constexpr int QP = (QW + PH - 1) / PH;
+    static constexpr int RS = QP * 4 + (QP % 2 == 0 ? 4 : 0);  // == 4 mod 8 dwords
+    static constexpr int FLOATS = WAVE * RS;
+};
+
+// RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
+// Indices are compile-time after unrolling, so the window test folds away and
+// values outside the window are never computed.
+template <int LO, int HI>
+struct WindowSink {
+    float *row;
+    float b0, b1, b2, b3;
+    int idx;
+    __device__ void put(float v)
+    {
+        if (idx >= LO && idx < HI) {
+            switch (idx & 3) {
+            case 0: b0 = v; break;
+            case 1: b1 = v; break;
+            case 2: b2 = v; break;
+            default: b3 = v; store_f4(row + ((idx & ~3) - LO), b0, b1, b2, b3); break;
+            }
+        }
+        idx++;
+    }
+    __device__ void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    __device__ void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+    __device__ void finish() { while (idx & 3) put(0.f); }
+};
+
+// Value of `x` in lane (lane & ~(G-1)) + J: DPP quad_perm, G = 2 or 4.
+template <int G, int J, class T>
+__device__ __forceinline__ T lane_bcast(const T &x)
+{
+    static_assert(sizeof(T) % 4 == 0, "32-bit words");
+    static_assert(G == 2 || G == 4, "quad groups");
+    constexpr int NW = sizeof(T) / 4;
+    constexpr int CTRL = G == 4 ? J * 0x55 : (J | (J << 2) | ((J + 2) << 4) | ((J + 2) << 6));
+    int in[NW], out[NW];
+    __builtin_memcpy(in, &x, sizeof(T));
+#pragma unroll
+    for (int q = 0; q < NW; q++) out[q] = __builtin_amdgcn_update_dpp(0, in[q], CTRL, 0xF, 0xF, false);
+    T r;
+    __builtin_memcpy(&r, out, sizeof(T));
+    return r;
+}
+
+template <int G, class T, int J = 0>
+__device__ __forceinline__ void lane_gather(const T &mine, T (&out)[G])
+{
+    out[J] = lane_bcast<G, J>(mine);
+    if constexpr (J + 1 < G) lane_gather<G, T, J + 1>(mine, out);
+}
+
+// Agent policy of the agent-lane kernel (see EachAgent in bb_sim.h).  Called
+// at the top level of step_world_pre_obs, where the N lanes of a world are
+// converged.
+template <int G>
+struct LaneAgents {
+    int k;
+    template <class T, int N, class F>
+    __device__ void all(F f, T (&out)[N]) const
+    {
+        static_assert(N == G, "one lane per agent");
+        lane_gather<G>(f(k), out);
+    }
+};
+
+// Copy the wave's 64 staged rows (tile row r -> obs row row0 + r*row_stride)
+// as consecutive 16-byte pieces: tile piece q -> row piece Q0 + q, q < QN.
+// Rows whose bit is clear in `staged` were written directly or belong to no
+// world.
+template <int N, int QT, int RS, int Q0, int QN>
 __device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, int64_t row_stride,
                                            uint64_t staged, int lane)
 {
-    using T = ObsTile<N>;
     constexpr int OW = obs_width(N);
-    for (int f = lane; f < WAVE * T::QW; f += WAVE) {
-        const int r = f / T::QW, q = f - r * T::QW;
-        if ((staged >> r) & 1ull) {
-            const float4 v = *(const float4 *)(tile + r * T::RS + 4 * q);
-            *(float4 *)(obs + (row0 + (int64_t)r * row_stride) * OW + 4 * q) = v;
+    for (int f = lane; f < WAVE * QT; f += WAVE) {
+        const int r = f / QT, q = f - r * QT;
+        if (q < QN && ((staged >> r) & 1ull)) {
+            const float4 v = *(const float4 *)(tile + r * RS + 4 * q);
+            *(float4 *)(obs + (row0 + (int64_t)r * row_stride) * OW + 4 * (Q0 + q)) = v;
         }
     }
+}
+
+// MODE_TRACE: lane 0 of each wave records the constant-rate clock at the
+// phase boundaries (start, systems done, state stored, end).
+constexpr int TRACE_POINTS = 4;
+template <int MODE>
+__device__ __forceinline__ void trace_point(const Params &p, int point)
+{
+    if constexpr (MODE == MODE_TRACE) {
+        const uint64_t t = wall_clock64();
+        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + point] = t;
+    }
+}
+
+struct Intrinsic {
+    float v[INTRINSIC];
+};
+
+// Pass PHASE of the lane's row into its tile row (shared path or fast path).
+template <int N, int PHASE>
+__device__ __forceinline__ void emit_phase(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
+                                           float *trow, int32_t ib)
+{
+    using T = PhasedTile<N>;
+    constexpr int LO = PHASE * T::QP * 4, HI = LO + T::QP * 4;
+    WindowSink<LO, HI> o;
+    o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+    if (share) emit_row_shared(v, c, sh, 0, o, ib);
+    else emit_row_fast(v, c, 0, o, ib);
+}
+
+template <int N, int MODE, int PHASE = 0>
+__device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
+                                           bool fast, float *tile, int64_t row0, int lane, int32_t ib)
+{
+    using T = PhasedTile<N>;
+    if (fast) emit_phase<N, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
+    __syncthreads();
+    constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
+    flush_tile<N, T::QP, T::RS, Q0, QN>(tile, c.p->c.obs, row0, 1, __ballot(fast), lane);
+    if constexpr (PHASE + 1 < T::PH) {
+        __syncthreads();
+        obs_phases<N, MODE, PHASE + 1>(v, c, sh, share, fast, tile, row0, lane, ib);
+    }
+}
+
+// One lane per agent: lane = (w - w0) * N + k.
+template <int N, int MODE>
+__device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
+{
+    constexpr int OW = obs_width(N);
+    const int lane = threadIdx.x;
+    const int k = lane % N;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
+    const LaneAgents<N> ag{k};
+
+    World<N> s;
+    Ctx c = make_ctx(p, w, k == 0);
+    World<N> v;  // the world with this lane's agent in slot 0
+    trace_point<MODE>(p, 0);
+    if (active) {
+        load_world(s, p, w);
+        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip);
+        else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
+    }
+    trace_point<MODE>(p, 1);
+    if (active) {
+        agent_view(s, v, k);
+        // reward + state columns first, so their stores drain while the
+        // observation row is built
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
+        store_world_agent(v, p, w * N + k, 0);
+        if (k == 0) store_world_shared(s, p, w);
+    }
+    trace_point<MODE>(p, 2);
+    if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
+
+    // intrinsic block of the lane's agent, exchanged with the world's lanes
+    const int32_t ib = active ? inbounder_id(s) : -1;
+    const bool share = active && obs_sharable(s);
+    SharedObs<N> sh;
+    if (active) {
+        Intrinsic mine, all[N];
+        {
+            ArraySink<INTRINSIC> o;
+            o.idx = 0;
+            emit_intrinsic(v, o, 0, attacking_hoop(v, c, 0));
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) mine.v[q] = o.v[q];
+        }
+        lane_gather<N>(mine, all);
+#pragma unroll
+        for (int t = 0; t < N; t++) {
+            const int src = view_source<N>(t, k);
+            const Intrinsic it = sel(t == 0, mine, pick_by<N>(src, [&](int j) { return all[j]; }));
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) sh.intr[t].v[q] = it.v[q];
+        }
+#pragma unroll
+        for (int t = 1; t < N; t++) {
+            const F3 to = v.pos(t) - v.pos(0);
+            const float l2 = len2(to);
+            const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
+            sh.rdir[0][t] = l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f);
+            sh.rlen[0][t] = bbm::sqrtf_(l2);
+        }
+    }
+    float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
+    const bool fast = active && canonical_slots(v, 0);
+    if constexpr (MODE == MODE_DIRECT_OBS) {
+        if (active) {
+            if (share) {
+                RowSink o;
+                o.row = grow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                emit_row_shared(v, c, sh, 0, o, ib);
+            } else if (fast) {
+                fill_obs_fast(v, c, 0, grow, ib);
+            } else {
+                fill_obs_slow(v, c, 0, grow, ib);
+            }
+        }
+    } else {
+        if (active && !fast) fill_obs_slow(v, c, 0, grow, ib);
+        obs_phases<N, MODE>(v, c, sh, share, fast, tile, w0 * N, lane, ib);
+    }
+    trace_point<MODE>(p, 3);
+}
+
+// One lane per world.
+template <int N, int MODE>
+__device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
+{
+    using T = ObsTile<N>;
+    const int lane = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * WAVE;
+    const int64_t w = w0 + lane;
+    const bool active = w < p.num_worlds;
+
+    World<N> s;
+    Ctx c = make_ctx(p, w, true);
+    trace_point<MODE>(p, 0);
+    if (active) {
+        load_world(s, p, w);
+        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, EachAgent(), p.diag_skip);
+        else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
+    }
+    trace_point<MODE>(p, 1);
+    if (active) {
+        // reward + state columns first, so their stores drain while the
+        // observation rows are built
+        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);
+        store_world(s, p, w);
+    }
+    trace_point<MODE>(p, 2);
+    if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
+        return;
+    } else if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
+        if (active) sys_fill_obs(s, c);
+    } else {
+        const int32_t ib = active ? inbounder_id(s) : -1;
+        const bool share = active && obs_sharable(s);
+        SharedObs<N> sh;
+        if (share) shared_obs_prepare(s, c, sh);
+#pragma unroll
+        for (int a = 0; a < N; a++) {
+            float *trow = tile + lane * T::RS;
+            const bool fast = active && (share || canonical_slots(s, a));
+            if (share) {
+                RowSink o;
+                o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                emit_row_shared(s, c, sh, a, o, ib);
+            } else if (fast) {
+                fill_obs_fast(s, c, a, trow, ib);
+            } else if (active) {
+                fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)obs_width(N), ib);
+            }
+            __syncthreads();
+            flush_tile<N, T::QW, T::RS, 0, T::QW>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
+            __syncthreads();
+        }
+    }
+    trace_point<MODE>(p, 3);
+}
+
+template <int N>
+constexpr int tile_floats()
+{
+    return Lanes<N>::LPW == N ? PhasedTile<N>::FLOATS : ObsTile<N>::FLOATS;
 }
 
 template <int N, int MODE>
 __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
-    using T = ObsTile<N>;
-    constexpr int LPW = Lanes<N>::LPW, WPB = Lanes<N>::WPB;
-    constexpr int OW = obs_width(N);
-    __shared__ float4 tile4[T::FLOATS / 4];
-    float *tile = (float *)tile4;
-    const int lane = threadIdx.x;
-    const int k = lane % LPW;  // this lane's agent when LPW == N
-    const int64_t w0 = (int64_t)blockIdx.x * WPB;
-    const int64_t w = w0 + lane / LPW;
-    const bool active = w < p.num_worlds;
-
-    World<N> s;
-    Ctx c = make_ctx(p, w, k == 0);
-    if (active) {
-        load_world(s, p, w);
-        if constexpr (MODE == MODE_SKIP) step_world_pre_obs_diag(s, c, p.diag_skip);
-        else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
-    }
-    // ---------------------------------------------------------- observations
-    // view of the world with this lane's agent in slot 0 (LPW == N)
-    World<N> v;
-    int32_t ib = -1;
-    if constexpr (LPW == N) {
-        if (active) {
-            ib = inbounder_id(s);
-            agent_view(s, v, k);
-        }
-    }
-    if constexpr (LPW != N && (MODE == MODE_IO || MODE == MODE_NO_OBS)) {
-        if (active) {
-            if constexpr (MODE == MODE_NO_OBS) sys_reward(s);
-            store_world(s, p, w);
-        }
-        return;
-    } else if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
-    } else if constexpr (LPW == N) {
-        float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
-        if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
-            if (active) {
-                if (canonical_slots(v, 0)) fill_obs_fast(v, c, 0, grow, ib);
-                else fill_obs_slow(v, c, 0, grow, ib);
-            }
-        } else {
-            const bool fast = active && canonical_slots(v, 0);
-            if (fast) fill_obs_fast(v, c, 0, tile + lane * T::RS, ib);
-            else if (active) fill_obs_slow(v, c, 0, grow, ib);
-            __syncthreads();
-            // lane = (w - w0) * N + k: the wave's rows are consecutive in memory
-            flush_tile<N>(tile, p.c.obs, w0 * N, 1, __ballot(fast), lane);
-        }
-    } else {
-        // one lane per world: reward + state columns first, so their stores
-        // drain while the observation rows are built
-        if (active) {
-            if constexpr (MODE != MODE_IO_OBS) sys_reward(s);
-            store_world(s, p, w);
-        }
-        if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
-            if (active) sys_fill_obs(s, c);
-        } else {
-            const int32_t ib1 = active ? inbounder_id(s) : -1;
-            const bool share = active && obs_sharable(s);
-            SharedObs<N> sh;
-            if (share) shared_obs_prepare(s, c, sh);
-#pragma unroll
-            for (int a = 0; a < N; a++) {
-                float *trow = tile + lane * T::RS;
-                const bool fast = active && (share || canonical_slots(s, a));
-                if (share) {
-                    RowSink o;
-                    o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
-                    emit_row_shared(s, c, sh, a, o, ib1);
-                } else if (fast) {
-                    fill_obs_fast(s, c, a, trow, ib1);
-                } else if (active) {
-                    fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)OW, ib1);
-                }
-                __syncthreads();
-                flush_tile<N>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
-                __syncthreads();
-            }
-        }
-        return;
-    }
-    // ---------------------------------------------------------- reward + store
-    if (!active) return;
-    if constexpr (LPW == N) {
-        if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
-        store_world_agent(v, p, w * N + k, 0);
-        if (k == 0) store_world_shared(s, p, w);
-    }
+    __shared__ float4 tile4[tile_floats<N>() / 4];
+    if constexpr (Lanes<N>::LPW == N) step_agent_lanes<N, MODE>(p, (float *)tile4);
+    else step_world_lanes<N, MODE>(p, (float *)tile4);
 }
 
 template <int N>
@@ -184,6 +361,7 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s)
     case MODE_DIRECT_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_DIRECT_OBS>), grid, block, 0, s, p); break;
     case MODE_NO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_NO_OBS>), grid, block, 0, s, p); break;
     case MODE_SKIP: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_SKIP>), grid, block, 0, s, p); break;
+    case MODE_TRACE: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_TRACE>), grid, block, 0, s, p); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -198,5 +376,6 @@ hipError_t launch_init_t(const Params &p, hipStream_t s)
 
 template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
+template <> int step_grid<BB_N>(int64_t num_worlds) { return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB); }
 
 }  // namespace bb

@@ -15,14 +15,17 @@ enum StepMode : int {
     MODE_DIRECT_OBS = 3,  // 19 systems, observation rows stored lane-strided (v1)
     MODE_NO_OBS = 4,      // systems 1-17 and 19, no observation rows
     MODE_SKIP = 5,        // full, minus the systems whose bit is set in Params::diag_skip
+    MODE_TRACE = 6,       // full, plus per-wave phase clocks into Params::diag_ts
 };
 
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
+template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)
 
 #define BB_EXTERN_N(n)                                                                  \
     extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t);      \
-    extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);
+    extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);           \
+    template <> int step_grid<n>(int64_t);
 BB_EXTERN_N(2)
 BB_EXTERN_N(4)
 BB_EXTERN_N(6)
@@ -32,6 +35,7 @@ BB_EXTERN_N(10)
 
 hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL);
 hipError_t launch_init(int n, const Params &p, hipStream_t s);
+int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)

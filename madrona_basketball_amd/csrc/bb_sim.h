@@ -12,6 +12,7 @@
 // for the build-internal state (velocity, cooldown, ...).  See DESIGN.md.
 #pragma once
 #include <stdint.h>
+#include <type_traits>
 #include "bb_math.h"
 #include "bb_rng.h"
 
@@ -144,6 +145,27 @@ BB_HD int32_t shot_point_value(F3 p, F3 hz)
     return d >= ARC ? 3 : 2;
 }
 
+// c ? a : b, word by word for aggregates (a ?: on structs selects between
+// their addresses, which leaves the operands in scratch memory).
+template <class T>
+BB_HD T sel(bool c, const T &a, const T &b)
+{
+    if constexpr (std::is_arithmetic<T>::value) {
+        return c ? a : b;
+    } else {
+        static_assert(sizeof(T) % 4 == 0, "32-bit words");
+        constexpr int NW = sizeof(T) / 4;
+        uint32_t x[NW], y[NW];
+        __builtin_memcpy(x, &a, sizeof(T));
+        __builtin_memcpy(y, &b, sizeof(T));
+#pragma unroll
+        for (int q = 0; q < NW; q++) x[q] = c ? x[q] : y[q];
+        T r;
+        __builtin_memcpy(&r, x, sizeof(T));
+        return r;
+    }
+}
+
 // Value of f(j) for j == i, built from selects (i may be a runtime value --
 // e.g. the lane's agent -- while every array index inside f stays constant).
 template <int N, class F>
@@ -151,12 +173,23 @@ BB_HD auto pick_by(int i, F f) -> decltype(f(0))
 {
     auto r = f(0);
 #pragma unroll
-    for (int j = 1; j < N; j++) {
-        auto x = f(j);
-        r = (i == j) ? x : r;
-    }
+    for (int j = 1; j < N; j++) r = sel(i == j, f(j), r);
     return r;
 }
+
+// How per-agent work is spread over lanes.  EachAgent: the calling lane
+// computes every agent's result (host executor, one lane per world).  The
+// agent-lane kernel (bb_kernels.hip) passes a policy that computes only the
+// lane's own agent and collects the others from the neighbouring lanes of
+// the same world.  f(i) may read anything but must not write the world.
+struct EachAgent {
+    template <class T, int N, class F>
+    BB_HD void all(F f, T (&out)[N]) const
+    {
+#pragma unroll
+        for (int i = 0; i < N; i++) out[i] = f(i);
+    }
+};
 
 // ------------------------------------------------------------------ layout
 // Column pointers.  Exported columns keep the reference byte layouts;
@@ -206,6 +239,7 @@ struct Params {
     float rot_thresh;            // (float)acos(c) > pi/8  <=>  c < rot_thresh   game.cpp:746-747
     int32_t rot_exact;           // 1: threshold not verified, evaluate acos
     uint32_t diag_skip;          // diagnostics only (MODE_SKIP): systems to leave out
+    uint64_t *diag_ts;           // diagnostics only (MODE_TRACE): TRACE_POINTS clocks per wave
 };
 
 BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
@@ -653,11 +687,13 @@ BB_HD void apply_move(World<N> &s, int j, const MoveOut &o)
     s.set_q(j, o.q); s.set_vel(j, o.vel); s.px[j] = o.px; s.py[j] = o.py;
 }
 
-template <int N>
-BB_HD void sys_move_agents(World<N> &s, const Ctx &c)
+template <int N, class A>
+BB_HD void sys_move_agents(World<N> &s, const Ctx &c, const A &ag)
 {
+    MoveOut o[N];  // agent i reads only its own columns
+    ag.all([&](int i) { return move_one(gather_move(s, i), *c.p); }, o);
 #pragma unroll
-    for (int i = 0; i < N; i++) apply_move(s, i, move_one(gather_move(s, i), *c.p));
+    for (int i = 0; i < N; i++) apply_move(s, i, o[i]);
 }
 
 template <int N>
@@ -794,12 +830,11 @@ BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
     return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)));
 }
 
-template <int N>
-BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c)
+template <int N, class A>
+BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c, const A &ag)
 {
-    float v[N];
-#pragma unroll
-    for (int i = 0; i < N; i++) v[i] = shot_pct_one(s, c, i);  // reads nothing it writes
+    float v[N];  // reads nothing it writes
+    ag.all([&](int i) { return shot_pct_one(s, c, i); }, v);
 #pragma unroll
     for (int i = 0; i < N; i++) s.attr[i][8] = v[i];
 }
@@ -912,11 +947,13 @@ BB_HD int32_t points_worth_one(const World<N> &s, const Ctx &c, int i)
     return 2;
 }
 
-template <int N>
-BB_HD void sys_points_worth(World<N> &s, const Ctx &c)
+template <int N, class A>
+BB_HD void sys_points_worth(World<N> &s, const Ctx &c, const A &ag)
 {
+    int32_t v[N];  // reads only pos/dhoop
+    ag.all([&](int i) { return points_worth_one(s, c, i); }, v);
 #pragma unroll
-    for (int i = 0; i < N; i++) s.pw[i] = points_worth_one(s, c, i);  // reads only pos/dhoop
+    for (int i = 0; i < N; i++) s.pw[i] = v[i];
 }
 
 struct Proj { float mn, mx; };
@@ -1048,12 +1085,13 @@ BB_HD void apply_defense(World<N> &s, int j, const DefOut &o)
     s.set_target(j, o.target);
 }
 
-template <int N>
-BB_HD void sys_defense(World<N> &s, const Ctx &c)
+template <int N, class A>
+BB_HD void sys_defense(World<N> &s, const Ctx &c, const A &ag)
 {
-    // agent i reads only fields no other agent's defence writes
+    DefOut o[N];  // agent i reads only fields no other agent's defence writes
+    ag.all([&](int i) { return defense_one(s, c, i); }, o);
 #pragma unroll
-    for (int i = 0; i < N; i++) apply_defense(s, i, defense_one(s, c, i));
+    for (int i = 0; i < N; i++) apply_defense(s, i, o[i]);
 }
 
 // ---- rewardSystem (game.cpp:811-870), one agent ------------------------
@@ -1240,11 +1278,9 @@ BB_HD bool canonical_slots(const World<N> &s, int a)
     return mates == N / 2 - 1 && opps == N / 2;
 }
 
-template <int N>
-BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
+template <int N, class Sink>
+BB_HD void emit_row_fast(const World<N> &s, const Ctx &c, int a, Sink &o, int32_t ib)
 {
-    RowSink o;
-    o.row = row; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
     F3 att, dfn;
     obs_header(s, c, o, a, &att, &dfn);
     const F3 p = s.pos(a);
@@ -1259,6 +1295,14 @@ BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row, int
 #pragma unroll
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
     o.finish();
+}
+
+template <int N>
+BB_HD void fill_obs_fast(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
+{
+    RowSink o;
+    o.row = row; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+    emit_row_fast(s, c, a, o, ib);
 }
 
 // Observation rows of every agent of a world with each agent's intrinsic
@@ -1389,61 +1433,31 @@ BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
 }
 
 // ------------------------------------------------------------------ one step
-// Systems 1-17 (everything before fillObservations).
-template <int N>
-BB_HD void step_world_pre_obs(World<N> &s, Ctx &c)
-{
-    const uint32_t flags = c.p->flags;
-    sys_tick(s);                                   // 1
-    sys_action_mask(s, flags);                     // 2
-    sys_move_agents(s, c);                         // 3
-#pragma unroll
-    for (int i = 0; i < N; i++) sys_grab(s, i);    // 4
-#pragma unroll
-    for (int i = 0; i < N; i++) sys_pass(s, i);    // 5
-#pragma unroll
-    for (int i = 0; i < N; i++) sys_shoot(s, c, i);  // 6
-    sys_move_ball(s, c);                           // 7
-    sys_shot_percentage(s, c);                     // 8
-    sys_score(s, c, 0);                            // 9 (hoop 0, then hoop 1)
-    sys_score(s, c, 1);
-    sys_out_of_bounds(s, c);                       // 10
-    sys_last_touch(s);                             // 11
-    sys_clock(s);                                  // 12
-    sys_inbound_violation(s, c);                   // 13
-    if (s.reset_now != 0) {                        // 14 resetSystem
-        reset_world(s, c);
-        s.reset_now = 0;
-    }
-    sys_points_worth(s, c);                        // 15
-    sys_collisions(s);                             // 16
-    sys_defense(s, c);                             // 17
-}
-
-// Diagnostic copy of systems 1-17 that leaves out the systems whose bit
-// (1 << system number) is set -- timing attribution only, not the game.
-template <int N>
-BB_HD void step_world_pre_obs_diag(World<N> &s, Ctx &c, uint32_t skip)
+// Systems 1-17 (everything before fillObservations).  `skip` leaves out the
+// systems whose bit (1 << system number) is set -- timing attribution only
+// (bb_diag_time); the game passes 0 and the tests fold away.
+template <int N, class A = EachAgent>
+BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t skip = 0)
 {
     const uint32_t flags = c.p->flags;
 #define BB_RUN(bit, stmt) if (!(skip & (1u << (bit)))) { stmt; }
     BB_RUN(1, sys_tick(s))
     BB_RUN(2, sys_action_mask(s, flags))
-    BB_RUN(3, sys_move_agents(s, c))
+    BB_RUN(3, sys_move_agents(s, c, ag))
     BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, i))
     BB_RUN(5, for (int i = 0; i < N; i++) sys_pass(s, i))
     BB_RUN(6, for (int i = 0; i < N; i++) sys_shoot(s, c, i))
     BB_RUN(7, sys_move_ball(s, c))
-    BB_RUN(8, sys_shot_percentage(s, c))
-    BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))
+    BB_RUN(8, sys_shot_percentage(s, c, ag))
+    BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))   // hoop 0, then hoop 1
     BB_RUN(10, sys_out_of_bounds(s, c))
     BB_RUN(11, sys_last_touch(s))
     BB_RUN(12, sys_clock(s))
     BB_RUN(13, sys_inbound_violation(s, c))
-    BB_RUN(14, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })
-    BB_RUN(15, sys_points_worth(s, c))
+    BB_RUN(14, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })  // resetSystem
+    BB_RUN(15, sys_points_worth(s, c, ag))
     BB_RUN(16, sys_collisions(s))
-    BB_RUN(17, sys_defense(s, c))
+    BB_RUN(17, sys_defense(s, c, ag))
 #undef BB_RUN
 }
 
@@ -1465,7 +1479,7 @@ BB_HD T pick(const T (&a)[N], int idx)
 {
     T r = a[0];
 #pragma unroll
-    for (int i = 1; i < N; i++) r = (idx == i) ? a[i] : r;
+    for (int i = 1; i < N; i++) r = sel(idx == i, a[i], r);
     return r;
 }
 

@@ -53,7 +53,32 @@ def main():
         out[MODES[m]] = {"median_us": med, "min_us": min(v), "algorithmic_GBps": B * args.worlds / (med * 1e-6) / 1e9}
         print(f"{MODES[m]:40s} median {med:8.2f} us  min {min(v):8.2f} us  "
               f"alg {out[MODES[m]]['algorithmic_GBps']:7.0f} GB/s", flush=True)
+    out["trace"] = trace(L, sim, stream)
     print(json.dumps({"worlds": args.worlds, "agents": args.agents, "results": out}))
+
+
+def trace(L, sim, stream):
+    """Per-wave phase clocks of one MODE_TRACE launch (wall_clock64 ticks,
+    100 MHz on gfx950): when waves start/end and how long each phase takes."""
+    import numpy as np
+    L.bb_diag_trace.restype = ctypes.c_int
+    L.bb_diag_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.POINTER(ctypes.c_int64)]
+    cap = 1 << 20
+    buf = np.zeros((cap, 4), dtype=np.uint64)
+    nw = ctypes.c_int64()
+    rc = L.bb_diag_trace(sim._h, stream, buf.ctypes.data, cap, ctypes.byref(nw))
+    assert rc == 0, L.bb_last_error()
+    t = buf[: nw.value].astype(np.int64)
+    t -= t[:, 0].min()
+    pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
+    res = {"waves": int(nw.value), "tick_ns": 10,
+           "start_pct": pct(t[:, 0]), "end_pct": pct(t[:, 3]),
+           "systems_pct": pct(t[:, 1] - t[:, 0]), "store_pct": pct(t[:, 2] - t[:, 1]),
+           "obs_pct": pct(t[:, 3] - t[:, 2]), "lifetime_pct": pct(t[:, 3] - t[:, 0])}
+    for k, v in res.items():
+        print(f"trace {k:14s} {v}", flush=True)
+    return res
 
 
 if __name__ == "__main__":

@@ -50,6 +50,7 @@ for s in $STEPS; do
     ablate) run ablate 600 python tools/ablate.py --worlds 65536 ;;
     ablate262k) run ablate262k 600 python tools/ablate.py --worlds 262144 --iters 50 ;;
     systems) run systems 600 python tools/ablate_systems.py --worlds 65536 ;;
+    pmcab) run pmcab 900 bash tools/pmc_ablate.sh "$TAG/pmc" 65536 ;;
     prof)
         ( cd /tmp && export TMPDIR=/tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run \
             --output-format csv -- python3 "$ROOT/bench.py" --steps 300 --warmup 30 --no-cpu-baseline ) || exit $?
