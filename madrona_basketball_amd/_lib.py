@@ -70,11 +70,13 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
+    # MADRONA_BB_LIB: a diagnostic variant build (build.py --variant), for A/B timing
+    path = os.environ.get("MADRONA_BB_LIB") or LIB_PATH
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -m madrona_basketball_amd.build` "
+            f"{path} is missing: build it with `python -m madrona_basketball_amd.build` "
             "(hipcc --offload-arch=gfx950). There is no Python fallback.")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, i32, i64, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32
     cfgp = ctypes.POINTER(Config)
     sig = {

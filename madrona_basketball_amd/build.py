@@ -48,33 +48,45 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = False, variant: str | None = None,
+          defines: list[str] | None = None) -> str:
+    """Build the library; a `variant` (diagnostics: A/B timing of compile-time
+    alternatives) goes to _variants/<variant>/ with extra -D `defines` and is
+    loaded only when MADRONA_BB_LIB points at it."""
+    lib_path = LIB_PATH if variant is None else os.path.join(HERE, "_variants", variant, LIB_NAME)
+    if variant is None and not force and not _stale():
         return LIB_PATH
     cc = hipcc()
     objs = []
-    build_dir = os.path.join(HERE, "_build")
+    build_dir = os.path.join(HERE, "_build" if variant is None else os.path.join("_variants", variant, "_build"))
     os.makedirs(build_dir, exist_ok=True)
     from concurrent.futures import ThreadPoolExecutor
     jobs = max(1, min(len(UNITS), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4))))
     cmds = []
     for src, extra, objname in UNITS:
         obj = os.path.join(build_dir, objname)
-        cmds.append([cc, *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj])
+        cmds.append([cc, *FLAGS, *extra, *[f"-D{d}" for d in (defines or [])], "-c", os.path.join(CSRC, src),
+                     "-o", obj])
         objs.append(obj)
         if verbose:
             print(" ".join(cmds[-1]), file=sys.stderr)
     with ThreadPoolExecutor(jobs) as ex:
         for r in ex.map(lambda c: subprocess.run(c), cmds):
             r.check_returncode()
-    tmp = LIB_PATH + ".tmp"
+    tmp = lib_path + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("--variant", default=None, help="diagnostic build under _variants/<name>/")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a variant")
+    a = ap.parse_args()
+    print(build(force=a.force, verbose=True, variant=a.variant, defines=a.defines))

@@ -87,14 +87,29 @@ struct WindowSink {
     __device__ void finish() { while (idx & 3) put(0.f); }
 };
 
-// Value of `x` in lane (lane & ~(G-1)) + J: DPP quad_perm, G = 2 or 4.
-template <int G, int J, class T>
-__device__ __forceinline__ T lane_bcast(const T &x)
+// DPP quad_perm controls: lane k of each G-lane group (G = 2, 4) reads
+// lane J of its group (bcast), or the lane of the agent in slot T of lane
+// k's agent view (view).
+template <int G, int J>
+constexpr int bcast_ctrl()
+{
+    int c = 0;
+    for (int l = 0; l < 4; l++) c |= ((l / G) * G + J) << (2 * l);
+    return c;
+}
+template <int G, int T>
+constexpr int view_ctrl()
+{
+    int c = 0;
+    for (int l = 0; l < 4; l++) c |= ((l / G) * G + view_source<G>(T, l % G)) << (2 * l);
+    return c;
+}
+
+template <int CTRL, class T>
+__device__ __forceinline__ T lane_dpp(const T &x)
 {
     static_assert(sizeof(T) % 4 == 0, "32-bit words");
-    static_assert(G == 2 || G == 4, "quad groups");
     constexpr int NW = sizeof(T) / 4;
-    constexpr int CTRL = G == 4 ? J * 0x55 : (J | (J << 2) | ((J + 2) << 4) | ((J + 2) << 6));
     int in[NW], out[NW];
     __builtin_memcpy(in, &x, sizeof(T));
 #pragma unroll
@@ -104,11 +119,32 @@ __device__ __forceinline__ T lane_bcast(const T &x)
     return r;
 }
 
+// Value of `x` in lane (lane & ~(G-1)) + J.
+template <int G, int J, class T>
+__device__ __forceinline__ T lane_bcast(const T &x)
+{
+    static_assert(G == 2 || G == 4, "quad groups");
+    return lane_dpp<bcast_ctrl<G, J>()>(x);
+}
+
+// out[j] = agent j's value (creation order), from the world's G lanes.
 template <int G, class T, int J = 0>
 __device__ __forceinline__ void lane_gather(const T &mine, T (&out)[G])
 {
     out[J] = lane_bcast<G, J>(mine);
     if constexpr (J + 1 < G) lane_gather<G, T, J + 1>(mine, out);
+}
+
+// out[t] = value of the agent in slot t of this lane's agent view
+// (view_source): slot 0 is the lane itself, one DPP per further slot.
+template <int G, class T, int J = 1>
+__device__ __forceinline__ void lane_gather_view(const T &mine, T (&out)[G])
+{
+    if constexpr (J == 1) out[0] = mine;
+    if constexpr (J < G) {
+        out[J] = lane_dpp<view_ctrl<G, J>()>(mine);
+        lane_gather_view<G, T, J + 1>(mine, out);
+    }
 }
 
 // Agent policy of the agent-lane kernel (see EachAgent in bb_sim.h).  Called
@@ -125,33 +161,68 @@ struct LaneAgents {
     }
 };
 
-// Copy the wave's 64 staged rows (tile row r -> obs row row0 + r*row_stride)
-// as consecutive 16-byte pieces: tile piece q -> row piece Q0 + q, q < QN.
+// Copy the wave's 64 staged rows (tile row r -> obs row row0 + r*RSTR) as
+// consecutive 16-byte pieces: tile piece q -> row piece Q0 + q, q < QN.
 // Rows whose bit is clear in `staged` were written directly or belong to no
-// world.
-template <int N, int QT, int RS, int Q0, int QN>
-__device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, int64_t row_stride,
-                                           uint64_t staged, int lane)
+// world.  Pieces f = it*64 + lane: every LDS read of a batch is issued before
+// its stores, addresses are 32-bit offsets from the wave's first row.
+typedef float vf4 __attribute__((ext_vector_type(4)));  // plain 16-byte loads/stores
+
+template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL>
+__device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64_t staged, int lane)
 {
     constexpr int OW = obs_width(N);
-    for (int f = lane; f < WAVE * QT; f += WAVE) {
-        const int r = f / QT, q = f - r * QT;
-        if (q < QN && ((staged >> r) & 1ull)) {
-            const float4 v = *(const float4 *)(tile + r * RS + 4 * q);
-            *(float4 *)(obs + (row0 + (int64_t)r * row_stride) * OW + 4 * (Q0 + q)) = v;
+    constexpr int DR = WAVE / QT, DQ = WAVE % QT;  // advance of f by 64
+    constexpr int BS = QT <= 16 ? QT : (QT + 1) / 2;
+    int r = lane / QT, q = lane - (lane / QT) * QT;
+#pragma unroll
+    for (int b0 = 0; b0 < QT; b0 += BS) {
+        vf4 v[BS];
+        uint32_t go[BS];
+        bool ok[BS];
+#pragma unroll
+        for (int j = 0; j < BS; j++) {
+            if (b0 + j < QT) {
+                ok[j] = (QN == QT || q < QN) && (ALL || ((staged >> r) & 1ull));
+                go[j] = (uint32_t)(r * (RSTR * OW * 4) + q * 16);
+                if (ok[j]) v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
+                r += DR;
+                q += DQ;
+                if (q >= QT) { q -= QT; r += 1; }
+            }
         }
+#pragma unroll
+        for (int j = 0; j < BS; j++)
+            if (b0 + j < QT && ok[j]) *(vf4 *)(base + go[j]) = v[j];
     }
 }
 
+template <int N, int QT, int RS, int Q0, int QN, int RSTR>
+__device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane)
+{
+    char *base = (char *)(obs + row0 * obs_width(N) + 4 * Q0);  // wave-uniform
+    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true>(tile, base, staged, lane);
+    else flush_rows<N, QT, RS, Q0, QN, RSTR, false>(tile, base, staged, lane);
+}
+
 // MODE_TRACE: lane 0 of each wave records the constant-rate clock at the
-// phase boundaries (start, systems done, state stored, end).
-constexpr int TRACE_POINTS = 4;
+// phase boundaries (start, systems done, state stored, end) and, in slot 4,
+// how many of the wave's lanes belong to a world that was reset this step.
+constexpr int TRACE_POINTS = 5;
 template <int MODE>
 __device__ __forceinline__ void trace_point(const Params &p, int point)
 {
     if constexpr (MODE == MODE_TRACE) {
         const uint64_t t = wall_clock64();
         if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + point] = t;
+    }
+}
+template <int MODE, int N>
+__device__ __forceinline__ void trace_resets(const Params &p, bool active, const World<N> &s)
+{
+    if constexpr (MODE == MODE_TRACE) {
+        const uint64_t m = __ballot(active && s.done[0] != 0.f);  // resetWorld sets Done = 1
+        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + 4] = (uint64_t)__popcll(m);
     }
 }
 
@@ -180,7 +251,7 @@ __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, cons
     if (fast) emit_phase<N, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     __syncthreads();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
-    flush_tile<N, T::QP, T::RS, Q0, QN>(tile, c.p->c.obs, row0, 1, __ballot(fast), lane);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1>(tile, c.p->c.obs, row0, __ballot(fast), lane);
     if constexpr (PHASE + 1 < T::PH) {
         __syncthreads();
         obs_phases<N, MODE, PHASE + 1>(v, c, sh, share, fast, tile, row0, lane, ib);
@@ -209,6 +280,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
     }
     trace_point<MODE>(p, 1);
+    trace_resets<MODE>(p, active, s);
     if (active) {
         agent_view(s, v, k);
         // reward + state columns first, so their stores drain while the
@@ -225,7 +297,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     const bool share = active && obs_sharable(s);
     SharedObs<N> sh;
     if (active) {
-        Intrinsic mine, all[N];
+        Intrinsic mine, slot[N];
         {
             ArraySink<INTRINSIC> o;
             o.idx = 0;
@@ -233,14 +305,11 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 #pragma unroll
             for (int q = 0; q < INTRINSIC; q++) mine.v[q] = o.v[q];
         }
-        lane_gather<N>(mine, all);
+        lane_gather_view<N>(mine, slot);
 #pragma unroll
-        for (int t = 0; t < N; t++) {
-            const int src = view_source<N>(t, k);
-            const Intrinsic it = sel(t == 0, mine, pick_by<N>(src, [&](int j) { return all[j]; }));
+        for (int t = 0; t < N; t++)
 #pragma unroll
-            for (int q = 0; q < INTRINSIC; q++) sh.intr[t].v[q] = it.v[q];
-        }
+            for (int q = 0; q < INTRINSIC; q++) sh.intr[t].v[q] = slot[t].v[q];
 #pragma unroll
         for (int t = 1; t < N; t++) {
             const F3 to = v.pos(t) - v.pos(0);
@@ -290,6 +359,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
     trace_point<MODE>(p, 1);
+    trace_resets<MODE>(p, active, s);
     if (active) {
         // reward + state columns first, so their stores drain while the
         // observation rows are built
@@ -320,7 +390,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
                 fill_obs_slow(s, c, a, p.c.obs + (w * N + a) * (int64_t)obs_width(N), ib);
             }
             __syncthreads();
-            flush_tile<N, T::QW, T::RS, 0, T::QW>(tile, p.c.obs, w0 * N + a, N, __ballot(fast), lane);
+            flush_tile<N, T::QW, T::RS, 0, T::QW, N>(tile, p.c.obs, w0 * N + a, __ballot(fast), lane);
             __syncthreads();
         }
     }

@@ -1484,7 +1484,7 @@ BB_HD T pick(const T (&a)[N], int idx)
 }
 
 template <int N>
-BB_HD int view_source(int slot, int k)  // absolute agent held by view slot
+BB_HD constexpr int view_source(int slot, int k)  // absolute agent held by view slot
 {
     return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
 }

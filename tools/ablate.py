@@ -65,17 +65,25 @@ def trace(L, sim, stream):
     L.bb_diag_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.POINTER(ctypes.c_int64)]
     cap = 1 << 20
-    buf = np.zeros((cap, 4), dtype=np.uint64)
+    buf = np.zeros((cap, 5), dtype=np.uint64)
     nw = ctypes.c_int64()
     rc = L.bb_diag_trace(sim._h, stream, buf.ctypes.data, cap, ctypes.byref(nw))
     assert rc == 0, L.bb_last_error()
-    t = buf[: nw.value].astype(np.int64)
+    t = buf[: nw.value, :4].astype(np.int64)
+    resets = buf[: nw.value, 4].astype(np.int64)
     t -= t[:, 0].min()
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
     res = {"waves": int(nw.value), "tick_ns": 10,
            "start_pct": pct(t[:, 0]), "end_pct": pct(t[:, 3]),
            "systems_pct": pct(t[:, 1] - t[:, 0]), "store_pct": pct(t[:, 2] - t[:, 1]),
-           "obs_pct": pct(t[:, 3] - t[:, 2]), "lifetime_pct": pct(t[:, 3] - t[:, 0])}
+           "obs_pct": pct(t[:, 3] - t[:, 2]), "lifetime_pct": pct(t[:, 3] - t[:, 0]),
+           "waves_with_reset": int((resets > 0).sum()), "reset_lanes": int(resets.sum())}
+    life = t[:, 3] - t[:, 0]
+    sysd = t[:, 1] - t[:, 0]
+    for name, sel in (("reset", resets > 0), ("no_reset", resets == 0)):
+        if sel.any():
+            res[f"lifetime_{name}_pct"] = pct(life[sel])
+            res[f"systems_{name}_pct"] = pct(sysd[sel])
     for k, v in res.items():
         print(f"trace {k:14s} {v}", flush=True)
     return res
