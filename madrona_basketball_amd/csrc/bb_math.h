@@ -222,7 +222,7 @@ BB_HD double exp_d(double x)
 
 // Maclaurin coefficients of erf(x) sqrt(pi)/(2x) in z = x^2: (-1)^n / (n! (2n+1)),
 // folded at compile time (identical on host and device).
-static constexpr int ERF_NT = 56;
+static constexpr int ERF_NT = 17;  // z <= 0.5625: term 17 < 1e-19
 struct ErfCoef {
     double c[ERF_NT];
     constexpr ErfCoef() : c()
@@ -236,26 +236,49 @@ struct ErfCoef {
 };
 static constexpr ErfCoef ERF_COEF{};
 
-// erf: Maclaurin series (Horner in x^2) below 3, 1 - erfc by the Laplace
-// continued fraction from 3 to 6, 1 above.  Absolute error < 1e-12 (the
-// reference only rounds it to float, src/game.cpp:808).
+// erf Taylor coefficients at c_k = 0.875 + k/4 (k = 0..12), degree 16
+static constexpr int ERF_TK = 13, ERF_TD = 16;
+static constexpr double ERF_TAYLOR[13][17] = {
+    {0.7840750610598597, 0.5247450452901482, -0.45915191462887966, 0.09292360177013041, 0.11239656243519451, -0.0672158773833572, -0.010367785745906018, 0.018595726765847267, -0.0018461468559063715, -0.0032568627602662854, 0.000898154868541066, 0.0003900529044120407, -0.00019296678621782653, -2.903116273391371e-05, 2.9075064952881173e-05, 2.0224352255317938e-07, -3.4142112964487243e-06},
+    {0.8883882317017078, 0.3182739585007693, -0.35805820331336546, 0.16245233298476766, 0.027973297133856677, -0.061323683605665806, 0.015536835449762896, 0.009606894225829976, -0.006031260883106729, -0.0003601919898013683, 0.0011532673547020597, -0.0001769550878579247, -0.0001415583990117997, 4.9455696834570095e-05, 1.0718804636659436e-05, -7.730906970255213e-06, -1.633684149181282e-07},
+    {0.9481700727820903, 0.1703597736875156, -0.23424468882033395, 0.15793770685613426, -0.03050061052348098, -0.030605976268925736, 0.022161235262852557, -0.001419062360662139, -0.004261033441276509, 0.001577911232741016, 0.00032359146722315554, -0.0003391015230725006, 2.8681755518788118e-05, 4.175471522740388e-05, -1.1984028581486832e-05, -2.9725595025012275e-06, 1.909045332332529e-06},
+    {0.9784437332399837, 0.08047225902251116, -0.13076742091158064, 0.11484061964670864, -0.049718863159090555, -0.0021349248406037306, 0.014414781131084502, -0.006184261515478821, -0.000576525430283408, 0.0014106850333898903, -0.00035597922602355293, -0.00012566368868411414, 8.79701620524859e-05, -4.270738262797687e-06, -1.0609039547562964e-05, 2.8273833059374034e-06, 6.634090465304774e-07},
+    {0.9919900576701199, 0.03354582842421607, -0.06289842829540514, 0.0674410925611844, -0.04225988151097533, 0.011462583364876176, 0.004105187133212477, -0.004928393908239107, 0.001430501687370122, 0.00036225644575338666, -0.0003901575782455417, 7.37299378240623e-05, 3.607417901263836e-05, -2.0803824921141647e-05, 8.154185088040366e-07, 2.3718570297022424e-06, -6.51036150696934e-07},
+    {0.9973459706405177, 0.012340820614333696, -0.026224243805459103, 0.033037405186289164, -0.026360828408612536, 0.012495482591433906, -0.0018214125933023405, -0.0018692572567887945, 0.0013833456162338344, -0.0002897798521792673, -0.00012277167237649306, 9.485303104752515e-05, -1.4992013287438935e-05, -8.475474393501074e-06, 4.549880654612466e-06, -2.397884034210181e-07, -4.671256150460798e-07},
+    {0.9992170617821089, 0.004006477861670219, -0.009515384921466771, 0.013730533505098981, -0.013133213563482782, 0.00835739283377895, -0.0031140790431462596, 0.0001232696283780691, 0.0005941113102532914, -0.00033752784148497275, 5.4705936215888043e-05, 3.1608810695225705e-05, -2.0800599114722e-05, 3.1425661169499264e-06, 1.6767083573168686e-06, -9.200372609631897e-07, 7.752008682814561e-08},
+    {0.9997946242638588, 0.001147875125882675, -0.003013172205442022, 0.004890426317562647, -0.005414293806653633, 0.004217880601717521, -0.0022468338447285286, 0.0006808680974231771, 3.464470636501039e-05, -0.00015260043098965162, 7.395616736023192e-05, -1.0326282078167697e-05, -6.687731493867075e-06, 4.157085191239199e-06, -6.770082881827777e-07, -2.7773383709897626e-07, 1.701157155860923e-07},
+    {0.9999521451602562, 0.00029022828286249803, -0.0008344063132296819, 0.001502536006069391, -0.001881760070981522, 0.0017132632798079331, -0.0011400746242208634, 0.0005285700413700108, -0.00013560801204451028, -1.6139055904620542e-05, 3.338804817529197e-05, -1.4811906943601079e-05, 2.0385768990676424e-06, 1.1871804277151051e-06, -7.564152887325688e-07, 1.429749505827574e-07, 3.6866827486454585e-08},
+    {0.9999901032653747, 6.475868323471298e-05, -0.00020237088510847805, 0.0004000197828977583, -0.0005575739490749213, 0.0005769615014743242, -0.00045231517761577534, 0.00026648105109162697, -0.00011126364024766743, 2.5450656904174918e-05, 3.873542145587109e-06, -6.36552916703948e-06, 2.7284794494107734e-06, -4.1406613481371433e-07, -1.7494853479255093e-07, 1.241605538071656e-07, -2.8089553938459793e-08},
+    {0.9999981847185726, 1.2751740799765088e-05, -4.303712519920718e-05, 9.258295143162778e-05, -0.00014188802214113615, 0.00016377394446104548, -0.0001464088816143732, 0.0001021861966850395, -5.484627167849354e-05, 2.126516551455692e-05, -4.603538423927069e-06, -6.548557786086127e-07, 1.0658621972744764e-06, -4.6107699262719935e-07, 8.175172180466655e-08, 2.0297448084600926e-08, -1.8100686787902113e-08},
+    {0.9999997048598075, 2.2159202846331124e-06, -8.032711031795032e-06, 1.8673744898626958e-05, -3.1168592284829685e-05, 3.959233534341495e-05, -3.952911393067182e-05, 3.151412148928749e-05, -2.0089148185951398e-05, 1.0055179082432725e-05, -3.7186007128168107e-06, 8.055029835948156e-07, 7.676629783825506e-08, -1.5640854840393676e-07, 7.087425570853251e-08, -1.4891022361493784e-08, -1.5211686584435892e-09},
+    {0.999999957486056, 3.398223817809154e-07, -1.3168117294010471e-06, 3.2884895070257334e-06, -5.9325111767286764e-06, 8.208845471821727e-06, -9.021089087308752e-06, 8.033147329562849e-06, -5.849020956804992e-06, 3.4746560653893003e-06, -1.6530325028002647e-06, 5.960564526364828e-07, -1.3449365553980958e-07, -3.880333287181606e-09, 1.9883468745269102e-08, -9.792703301880837e-09, 2.4236026415671354e-09},
+};
+
+// erf: Maclaurin series (Horner in x^2) below 0.75; Taylor polynomials at the
+// centres of 13 quarter-unit intervals on [0.75, 4) (no cancellation: every
+// value there is > 0.7); 1 from 4 on, where erfc < 2^-25 and the float result
+// is 1.  Absolute error ~2e-16 (the reference rounds erf to float,
+// src/game.cpp:808).
 BB_HD double erf_d(double x)
 {
     if (isnan_d(x)) return x;
     const double ax = fabs_d(x);
     double r;
-    if (ax < 3.0) {
+    if (ax < 0.75) {
         // erf x = 2/sqrt(pi) * x * sum_n (-1)^n z^n / (n! (2n+1)), z = x^2
         const double z = ax * ax;
         double p = ERF_COEF.c[ERF_NT - 1];
 #pragma unroll
         for (int n = ERF_NT - 2; n >= 0; n--) p = fma_d(p, z, ERF_COEF.c[n]);
         r = TWO_OVER_SQRTPI * (ax * p);
-    } else if (ax < 6.0) {
-        // erfc x = exp(-x^2)/sqrt(pi) * 1/(x + (1/2)/(x + 1/(x + (3/2)/(x + ...))))
-        double f = ax;
-        for (int k = 40; k >= 1; k--) f = ax + (0.5 * (double)k) / f;
-        r = 1.0 - exp_d(-(ax * ax)) * INV_SQRTPI / f;
+    } else if (ax < 4.0) {
+        const int k = (int)((ax - 0.75) * 4.0);
+        const double t = ax - (0.875 + 0.25 * (double)k);  // exact, |t| <= 1/8
+        const double *a = ERF_TAYLOR[k];
+        double p = a[ERF_TD];
+#pragma unroll
+        for (int n = ERF_TD - 1; n >= 0; n--) p = fma_d(p, t, a[n]);
+        r = p;
     } else {
         r = 1.0;
     }

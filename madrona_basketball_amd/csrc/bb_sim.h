@@ -380,6 +380,16 @@ BB_HD Ctx make_ctx(const Params &p, int64_t w, bool writer = true)
     Ctx c; c.p = &p; c.w = w; c.writer = writer; return c;
 }
 
+// sampleUniform at stream position ctr of the world's stream
+template <int N>
+BB_HD float sample_uniform_at(const World<N> &s, const Ctx &c, uint32_t ctr, float lo, float hi)
+{
+    const uint32_t k = (c.p->flags & FLAG_PER_WORLD_RNG) ? (uint32_t)(c.p->world_offset + c.w) : 0u;
+    uint32_t r0, r1;
+    threefry2x32(c.p->seed, k, ctr, 0u, &r0, &r1);
+    return lo + (hi - lo) * u01_from_bits(r0);
+}
+
 template <int N>
 BB_HD float sample_uniform(World<N> &s, Ctx &c, float lo, float hi)
 {
@@ -737,57 +747,127 @@ BB_HD void sys_pass(World<N> &s, int i)  // game.cpp:243-270
     }
 }
 
+// ---- shootSystem (game.cpp:273-407), one agent --------------------------
+// Agents shoot in creation order and draw 1-3 uniforms each from the world's
+// stream; only the ball holder's shot touches the ball, and no agent's shot
+// changes what a later agent reads except the stream position.  So agent i
+// is computed on its own from the counter after agents 0..i-1's draws.
 template <int N>
-BB_HD void sys_shoot(World<N> &s, Ctx &c, int i)  // game.cpp:273-407
+BB_HD float nearest_opponent(const World<N> &s, int i)  // game.cpp:311-322
 {
-    if (s.msk[i][3] == 0 || s.act[i][5] == 0) return;
-    const F3 pos = s.pos(i);
-    // attacking hoop: the last hoop (creation order) that is not defended
-    F3 target = f3(0.f, 0.f, 0.f);
-    float radius = 0.f;
-    if (HOOP0_ID != s.dhoop[i]) { target = hoop_pos<N>(c, 0); radius = HOOP_ZONE; }
-    if (HOOP1_ID != s.dhoop[i]) { target = hoop_pos<N>(c, 1); radius = HOOP_ZONE; }
-    const F3 ideal = target - pos;
-    const float intended = bbm::atan2f_(ideal.x, ideal.y);
-    const float dstd = DIST_DEV * len(ideal);
-    const float dev_d = sample_uniform(s, c, -dstd, dstd);
-    float dev_def = 0.0f;
+    const F3 pos = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const int32_t team = pick_by<N>(i, [&](int j) { return s.team[j]; });
     float nd = __builtin_inff();
 #pragma unroll
     for (int j = 0; j < N; j++) {
-        if (s.team[j] != s.team[i]) {
+        if (s.team[j] != team) {
             const float dd = len(pos - s.pos(j));
             if (dd < nd) nd = dd;
         }
     }
+    return nd;
+}
+
+template <int N>
+BB_HD bool shoots(const World<N> &s, int i)
+{
+    return s.msk[i][3] != 0 && s.act[i][5] != 0;
+}
+
+template <int N>
+BB_HD uint32_t shoot_draws(const World<N> &s, int i)  // uniforms agent i's shot consumes
+{
+    if (!shoots(s, i)) return 0u;
+    return 1u + (nearest_opponent(s, i) < 2.0f ? 1u : 0u) + (s.act[i][0] > 0 ? 1u : 0u);
+}
+
+struct ShootOut {
+    Q4 q;           // new orientation (shot == 1)
+    F3 fs;          // shot direction
+    int32_t shot;   // the agent shot this step
+    int32_t going;  // the shot goes in
+    int32_t value;  // point value of the holder's shot
+    int32_t pad;
+};
+
+template <int N>
+BB_HD ShootOut shoot_one(const World<N> &s, const Ctx &c, int i)
+{
+    ShootOut o;
+    o.q = pick_by<N>(i, [&](int j) { return s.q(j); });
+    o.fs = f3(0.f, 0.f, 0.f);
+    o.shot = 0; o.going = 0; o.value = 0; o.pad = 0;
+    const bool me = pick_by<N>(i, [&](int j) { return shoots(s, j); });
+    if (!me) return o;
+    uint32_t ctr = s.rng_ctr;
+#pragma unroll
+    for (int j = 0; j < N - 1; j++)
+        if (j < i) ctr += shoot_draws(s, j);
+    auto draw = [&](float lo, float hi) { return sample_uniform_at(s, c, ctr++, lo, hi); };
+    const F3 pos = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
+    // attacking hoop: the last hoop (creation order) that is not defended
+    F3 target = f3(0.f, 0.f, 0.f);
+    float radius = 0.f;
+    if (HOOP0_ID != dhoop) { target = hoop_pos<N>(c, 0); radius = HOOP_ZONE; }
+    if (HOOP1_ID != dhoop) { target = hoop_pos<N>(c, 1); radius = HOOP_ZONE; }
+    const F3 ideal = target - pos;
+    const float intended = bbm::atan2f_(ideal.x, ideal.y);
+    const float dstd = DIST_DEV * len(ideal);
+    const float dev_d = draw(-dstd, dstd);
+    float dev_def = 0.0f;
+    const float nd = nearest_opponent(s, i);
     if (nd < 2.0f) {
         const float sd = DEF_DEV / (nd + 0.1f);
-        dev_def = sample_uniform(s, c, -sd, sd);
+        dev_def = draw(-sd, sd);
     }
     float dev_v = 0.0f;
-    if (s.act[i][0] > 0) {
-        const float sv = VEL_DEV * len(s.vel(i));
-        dev_v = sample_uniform(s, c, -sv, sv);
+    if (pick_by<N>(i, [&](int j) { return s.act[j][0]; }) > 0) {
+        const float sv = VEL_DEV * len(pick_by<N>(i, [&](int j) { return s.vel(j); }));
+        dev_v = draw(-sv, sv);
     }
     const float dir = intended + ((dev_d + dev_def) + dev_v);
     float sn, cs;
     bbm::sincosf_(dir, &sn, &cs);
-    const F3 fs = f3(sn, cs, 0.f);
-    float going = 0.0f;
-    const float along = dot(ideal, fs);
-    if (!(along < 0.f)) going = (len2(ideal) - along * along <= radius * radius) ? 1.0f : 0.0f;
-    s.set_q(i, rotation_from_forward(fs));
+    o.fs = f3(sn, cs, 0.f);
+    const float along = dot(ideal, o.fs);
+    if (!(along < 0.f)) o.going = (len2(ideal) - along * along <= radius * radius) ? 1 : 0;
+    o.q = rotation_from_forward(o.fs);
+    o.shot = 1;
+    if (s.holder == AGENT0_ID + i) o.value = shot_point_value(pos, target);
+    return o;
+}
+
+template <int N>
+BB_HD void apply_shoot(World<N> &s, int i, const ShootOut &o)
+{
+    if (!o.shot) return;
+    s.set_q(i, o.q);
     if (s.holder == AGENT0_ID + i) {
-        const int32_t v = shot_point_value(pos, target);
-        if (going == 1.f) { s.gin = 1; s.g_bask += 1.f; }
+        if (o.going == 1) { s.gin = 1; s.g_bask += 1.f; }
         else s.rew[i] -= 1.f;
         s.grab = 0; s.holder = PH;
         s.has[i] = 0; s.bid[i] = PH; s.inb[i] = 0;
-        s.set_bvel(fs * .1f);
+        s.set_bvel(o.fs * .1f);
         s.fl = 1;
-        s.sba = AGENT0_ID + i; s.sbt = s.team[i]; s.spv = v;
+        s.sba = AGENT0_ID + i; s.sbt = s.team[i]; s.spv = o.value;
         s.lta = AGENT0_ID + i; s.ltt = s.team[i];
     }
+}
+
+template <int N, class A>
+BB_HD void sys_shoot(World<N> &s, const Ctx &c, const A &ag)
+{
+    ShootOut o[N];
+    ag.all([&](int i) { return shoot_one(s, c, i); }, o);
+    uint32_t draws = 0;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        draws += shoot_draws(s, i);  // before apply_shoot changes what it reads
+    }
+#pragma unroll
+    for (int i = 0; i < N; i++) apply_shoot(s, i, o[i]);
+    s.rng_ctr += draws;
 }
 
 template <int N>
@@ -876,7 +956,10 @@ BB_HD void sys_out_of_bounds(World<N> &s, Ctx &c)  // game.cpp:1055-1113
 {
     if (!((s.bx < CMINX || s.bx > CMAXX || s.by < CMINY || s.by > CMAXY) && (float)s.g_inb == 0.f)) return;
     if ((float)s.g_1v1 == 1.f) {
-        s.rew[offense_index(s)] -= 100.f;
+        const int off = offense_index(s);
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (i == off) s.rew[i] -= 100.f;  // register selects, not a runtime index
         s.reset_now = 1;
         return;
     }
@@ -908,7 +991,10 @@ BB_HD void sys_clock(World<N> &s)  // game.cpp:992-1030
     if ((float)s.g_live > 0.5f && s.g_clock > 0.f) { s.g_clock -= TS; s.g_shot -= TS; }
     if ((float)s.g_inb > 0.5f) s.g_inbclk -= TS;
     if (s.g_clock <= 0.f && (float)s.g_live > 0.5f) {
-        s.rew[offense_index(s)] += 10.f;
+        const int off = offense_index(s);
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (i == off) s.rew[i] += 10.f;
         s.reset_now = 1;
     }
     if (s.g_shot < 0.f) s.g_shot = 0.f;
@@ -1446,7 +1532,7 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t s
     BB_RUN(3, sys_move_agents(s, c, ag))
     BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, i))
     BB_RUN(5, for (int i = 0; i < N; i++) sys_pass(s, i))
-    BB_RUN(6, for (int i = 0; i < N; i++) sys_shoot(s, c, i))
+    BB_RUN(6, sys_shoot(s, c, ag))
     BB_RUN(7, sys_move_ball(s, c))
     BB_RUN(8, sys_shot_percentage(s, c, ag))
     BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))   // hoop 0, then hoop 1
