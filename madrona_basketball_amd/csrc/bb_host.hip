@@ -591,9 +591,8 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
 }
 
 // Diagnostic (not in the public header): one MODE_TRACE launch; copies the
-// per-wave phase clocks (wall_clock64 ticks: start, systems done, state
-// stored, end) and reset-lane count into out[waves][5].  *waves = number of
-// waves of the launch.
+// per-wave phase clocks and reset-lane count (bb_kernels.hip TRACE_POINTS)
+// into out[waves][12].  *waves = number of waves of the launch.
 int bb_diag_trace(bb_sim *s, void *stream, uint64_t *out, int64_t max_waves, int64_t *waves)
 {
     if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || !out || !waves) return fail(BB_ERR_INVALID_ARG, "bb_diag_trace");
@@ -603,10 +602,10 @@ int bb_diag_trace(bb_sim *s, void *stream, uint64_t *out, int64_t max_waves, int
     *waves = nw;
     if (nw > max_waves) return fail(BB_ERR_INVALID_ARG, "bb_diag_trace: out too small");
     bb::Params pp = s->p;
-    if (hipMalloc(&pp.diag_ts, (size_t)nw * 5 * sizeof(uint64_t)) != hipSuccess) return fail(BB_ERR_OOM, "trace buffer");
+    if (hipMalloc(&pp.diag_ts, (size_t)nw * 12 * sizeof(uint64_t)) != hipSuccess) return fail(BB_ERR_OOM, "trace buffer");
     hipError_t e = bb::launch_step(s->n, pp, st, bb::MODE_TRACE);  // warm
     if (e == hipSuccess) e = bb::launch_step(s->n, pp, st, bb::MODE_TRACE);
-    if (e == hipSuccess) e = hipMemcpyAsync(out, pp.diag_ts, (size_t)nw * 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(out, pp.diag_ts, (size_t)nw * 12 * sizeof(uint64_t), hipMemcpyDeviceToHost, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     (void)hipFree(pp.diag_ts);
     if (e != hipSuccess) return hip_fail(e, "diag trace");

@@ -147,18 +147,43 @@ __device__ __forceinline__ void lane_gather_view(const T &mine, T (&out)[G])
     }
 }
 
+// MODE_TRACE: lane 0 of each wave records the constant-rate clock at the
+// phase boundaries -- 0 start, 1 state loaded, 2-7 after groups of systems
+// (bb_sim.h step_world_pre_obs marks), 8 state stored, 9 end -- and in slot
+// 10 how many of the wave's lanes belong to a world reset this step.
+constexpr int TRACE_POINTS = 12;
+template <int MODE>
+__device__ __forceinline__ void trace_point(const Params &p, int point)
+{
+    if constexpr (MODE == MODE_TRACE) {
+        if (point == 1) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = wall_clock64();
+        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + point] = t;
+    }
+}
+template <int MODE, int N>
+__device__ __forceinline__ void trace_resets(const Params &p, bool active, const World<N> &s)
+{
+    if constexpr (MODE == MODE_TRACE) {
+        const uint64_t m = __ballot(active && s.done[0] != 0.f);  // resetWorld sets Done = 1
+        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + 10] = (uint64_t)__popcll(m);
+    }
+}
+
 // Agent policy of the agent-lane kernel (see EachAgent in bb_sim.h).  Called
 // at the top level of step_world_pre_obs, where the N lanes of a world are
 // converged.
-template <int G>
+template <int G, int MODE>
 struct LaneAgents {
     int k;
+    const Params *p;
     template <class T, int N, class F>
     __device__ void all(F f, T (&out)[N]) const
     {
         static_assert(N == G, "one lane per agent");
         lane_gather<G>(f(k), out);
     }
+    __device__ void mark(int point) const { trace_point<MODE>(*p, point); }
 };
 
 // Copy the wave's 64 staged rows (tile row r -> obs row row0 + r*RSTR) as
@@ -205,27 +230,6 @@ __device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_
     else flush_rows<N, QT, RS, Q0, QN, RSTR, false>(tile, base, staged, lane);
 }
 
-// MODE_TRACE: lane 0 of each wave records the constant-rate clock at the
-// phase boundaries (start, systems done, state stored, end) and, in slot 4,
-// how many of the wave's lanes belong to a world that was reset this step.
-constexpr int TRACE_POINTS = 5;
-template <int MODE>
-__device__ __forceinline__ void trace_point(const Params &p, int point)
-{
-    if constexpr (MODE == MODE_TRACE) {
-        const uint64_t t = wall_clock64();
-        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + point] = t;
-    }
-}
-template <int MODE, int N>
-__device__ __forceinline__ void trace_resets(const Params &p, bool active, const World<N> &s)
-{
-    if constexpr (MODE == MODE_TRACE) {
-        const uint64_t m = __ballot(active && s.done[0] != 0.f);  // resetWorld sets Done = 1
-        if (threadIdx.x == 0) p.diag_ts[(int64_t)blockIdx.x * TRACE_POINTS + 4] = (uint64_t)__popcll(m);
-    }
-}
-
 struct Intrinsic {
     float v[INTRINSIC];
 };
@@ -268,7 +272,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
     const int64_t w = w0 + lane / N;
     const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
-    const LaneAgents<N> ag{k};
+    const LaneAgents<N, MODE> ag{k, &p};
 
     World<N> s;
     Ctx c = make_ctx(p, w, k == 0);
@@ -279,7 +283,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
     }
-    trace_point<MODE>(p, 1);
+    trace_point<MODE>(p, 7);
     trace_resets<MODE>(p, active, s);
     if (active) {
         agent_view(s, v, k);
@@ -289,7 +293,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         store_world_agent(v, p, w * N + k, 0);
         if (k == 0) store_world_shared(s, p, w);
     }
-    trace_point<MODE>(p, 2);
+    trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
 
     // intrinsic block of the lane's agent, exchanged with the world's lanes
@@ -337,7 +341,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         if (active && !fast) fill_obs_slow(v, c, 0, grow, ib);
         obs_phases<N, MODE>(v, c, sh, share, fast, tile, w0 * N, lane, ib);
     }
-    trace_point<MODE>(p, 3);
+    trace_point<MODE>(p, 9);
 }
 
 // One lane per world.
@@ -358,7 +362,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, EachAgent(), p.diag_skip);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
-    trace_point<MODE>(p, 1);
+    trace_point<MODE>(p, 7);
     trace_resets<MODE>(p, active, s);
     if (active) {
         // reward + state columns first, so their stores drain while the
@@ -366,7 +370,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);
         store_world(s, p, w);
     }
-    trace_point<MODE>(p, 2);
+    trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {
         return;
     } else if constexpr (MODE == MODE_DIRECT_OBS || !T::STAGED) {
@@ -394,7 +398,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
             __syncthreads();
         }
     }
-    trace_point<MODE>(p, 3);
+    trace_point<MODE>(p, 9);
 }
 
 template <int N>
@@ -403,10 +407,28 @@ constexpr int tile_floats()
     return Lanes<N>::LPW == N ? PhasedTile<N>::FLOATS : ObsTile<N>::FLOATS;
 }
 
+// Start skew (timing experiment, off by default): wave group blockIdx % G
+// sleeps g * S s_sleep units before loading, so that groups sharing a SIMD
+// alternate between memory and compute phases instead of running in step.
+#ifndef BB_SKEW_G
+#define BB_SKEW_G 1
+#endif
+#ifndef BB_SKEW_S
+#define BB_SKEW_S 32
+#endif
+__device__ __forceinline__ void start_skew()
+{
+    if constexpr (BB_SKEW_G > 1) {
+        const int g = (int)(blockIdx.x % BB_SKEW_G);
+        for (int i = 0; i < g; i++) __builtin_amdgcn_s_sleep(BB_SKEW_S);
+    }
+}
+
 template <int N, int MODE>
 __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
     __shared__ float4 tile4[tile_floats<N>() / 4];
+    start_skew();
     if constexpr (Lanes<N>::LPW == N) step_agent_lanes<N, MODE>(p, (float *)tile4);
     else step_world_lanes<N, MODE>(p, (float *)tile4);
 }

@@ -182,6 +182,8 @@ BB_HD auto pick_by(int i, F f) -> decltype(f(0))
 // agent-lane kernel (bb_kernels.hip) passes a policy that computes only the
 // lane's own agent and collects the others from the neighbouring lanes of
 // the same world.  f(i) may read anything but must not write the world.
+// mark(point): timing hook between groups of systems (no-op here; the
+// kernel's trace variant records a clock).
 struct EachAgent {
     template <class T, int N, class F>
     BB_HD void all(F f, T (&out)[N]) const
@@ -189,6 +191,7 @@ struct EachAgent {
 #pragma unroll
         for (int i = 0; i < N; i++) out[i] = f(i);
     }
+    BB_HD void mark(int) const {}
 };
 
 // ------------------------------------------------------------------ layout
@@ -1527,20 +1530,26 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t s
 {
     const uint32_t flags = c.p->flags;
 #define BB_RUN(bit, stmt) if (!(skip & (1u << (bit)))) { stmt; }
+    ag.mark(1);
     BB_RUN(1, sys_tick(s))
     BB_RUN(2, sys_action_mask(s, flags))
     BB_RUN(3, sys_move_agents(s, c, ag))
+    ag.mark(2);
     BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, i))
     BB_RUN(5, for (int i = 0; i < N; i++) sys_pass(s, i))
     BB_RUN(6, sys_shoot(s, c, ag))
+    ag.mark(3);
     BB_RUN(7, sys_move_ball(s, c))
     BB_RUN(8, sys_shot_percentage(s, c, ag))
     BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))   // hoop 0, then hoop 1
+    ag.mark(4);
     BB_RUN(10, sys_out_of_bounds(s, c))
     BB_RUN(11, sys_last_touch(s))
     BB_RUN(12, sys_clock(s))
     BB_RUN(13, sys_inbound_violation(s, c))
+    ag.mark(5);
     BB_RUN(14, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })  // resetSystem
+    ag.mark(6);
     BB_RUN(15, sys_points_worth(s, c, ag))
     BB_RUN(16, sys_collisions(s))
     BB_RUN(17, sys_defense(s, c, ag))

@@ -65,25 +65,25 @@ def trace(L, sim, stream):
     L.bb_diag_trace.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.POINTER(ctypes.c_int64)]
     cap = 1 << 20
-    buf = np.zeros((cap, 5), dtype=np.uint64)
+    buf = np.zeros((cap, 12), dtype=np.uint64)
     nw = ctypes.c_int64()
     rc = L.bb_diag_trace(sim._h, stream, buf.ctypes.data, cap, ctypes.byref(nw))
     assert rc == 0, L.bb_last_error()
-    t = buf[: nw.value, :4].astype(np.int64)
-    resets = buf[: nw.value, 4].astype(np.int64)
+    t = buf[: nw.value, :10].astype(np.int64)
+    resets = buf[: nw.value, 10].astype(np.int64)
     t -= t[:, 0].min()
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
-    res = {"waves": int(nw.value), "tick_ns": 10,
-           "start_pct": pct(t[:, 0]), "end_pct": pct(t[:, 3]),
-           "systems_pct": pct(t[:, 1] - t[:, 0]), "store_pct": pct(t[:, 2] - t[:, 1]),
-           "obs_pct": pct(t[:, 3] - t[:, 2]), "lifetime_pct": pct(t[:, 3] - t[:, 0]),
-           "waves_with_reset": int((resets > 0).sum()), "reset_lanes": int(resets.sum())}
-    life = t[:, 3] - t[:, 0]
-    sysd = t[:, 1] - t[:, 0]
-    for name, sel in (("reset", resets > 0), ("no_reset", resets == 0)):
-        if sel.any():
-            res[f"lifetime_{name}_pct"] = pct(life[sel])
-            res[f"systems_{name}_pct"] = pct(sysd[sel])
+    names = ["load", "tick..move", "grab..shoot", "ball..score", "oob..inbound", "reset", "points..defense",
+             "reward+store", "obs"]
+    res = {"waves": int(nw.value), "tick_ns": 10, "start_pct": pct(t[:, 0]), "end_pct": pct(t[:, 9]),
+           "lifetime_pct": pct(t[:, 9] - t[:, 0]), "waves_with_reset": int((resets > 0).sum()),
+           "reset_lanes": int(resets.sum())}
+    for i, n in enumerate(names):
+        res[f"{n}_pct"] = pct(t[:, i + 1] - t[:, i])
+    sel = resets > 0
+    if sel.any() and (~sel).any():
+        res["reset_phase_with_reset_pct"] = pct(t[sel, 6] - t[sel, 5])
+        res["reset_phase_without_pct"] = pct(t[~sel, 6] - t[~sel, 5])
     for k, v in res.items():
         print(f"trace {k:14s} {v}", flush=True)
     return res
