@@ -7,17 +7,19 @@
 
 namespace bb {
 
-// one lane = one (world, agent) action row (24 B)
-__global__ __launch_bounds__(256) void k_random_actions(int32_t *action, int64_t rows, int32_t n,
-                                                        int64_t world_offset, uint32_t seed, uint32_t step)
+// one lane = one (world, agent) action row (24 B); N compile-time so the
+// row -> (world, agent) split is a multiply, not a 64-bit division
+template <int N>
+__global__ __launch_bounds__(256) void k_random_actions(int32_t *action, int32_t rows, int64_t world_offset,
+                                                        uint32_t seed, uint32_t step)
 {
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int32_t r = (int32_t)blockIdx.x * 256 + (int32_t)threadIdx.x;
     if (r >= rows) return;
-    const int64_t w = r / n;
-    const int32_t a = (int32_t)(r - w * n);
+    const int32_t w = r / N;
+    const int32_t a = r - w * N;
     int32_t act[6];
     random_action(seed, step, (uint32_t)(world_offset + w), (uint32_t)a, act);
-    int2 *dst = (int2 *)(action + r * 6);
+    int2 *dst = (int2 *)(action + (int64_t)r * 6);
     dst[0] = make_int2(act[0], act[1]);
     dst[1] = make_int2(act[2], act[3]);
     dst[2] = make_int2(act[4], act[5]);
@@ -46,10 +48,12 @@ __global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 
 
 static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
 
-hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s)
+template <int N>
+hipError_t launch_random_actions_t(const Params &p, uint32_t seed, uint32_t step, hipStream_t s)
 {
-    const int64_t rows = p.num_worlds * n;
-    hipLaunchKernelGGL(k_random_actions, grid_for(rows, 256), dim3(256), 0, s, p.c.action, rows, n,
+    const int64_t rows = p.num_worlds * N;
+    if (rows > INT32_MAX) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_random_actions<N>, grid_for(rows, 256), dim3(256), 0, s, p.c.action, (int32_t)rows,
                        p.world_offset, seed, step);
     return hipGetLastError();
 }
@@ -78,6 +82,13 @@ hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, in
     case 10: return call(10);                   \
     default: return hipErrorInvalidValue;       \
     }
+
+hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s)
+{
+#define CALL(k) launch_random_actions_t<k>(p, seed, step, s)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
 
 hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode)
 {

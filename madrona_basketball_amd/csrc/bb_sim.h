@@ -1059,9 +1059,20 @@ BB_HD Proj project(const F3 (&v)[4], F3 axis)  // helper.cpp:85-100
 }
 
 // Oriented-rectangle SAT contact between agents a < b (game.cpp:537-648).
+// Centres farther apart than the two circumscribed circles (+1% + 1 cm):
+// the rectangles are disjoint with a margin far above float rounding, so the
+// SAT test below finds a separating axis and changes nothing -- skip it.
+constexpr float COLLIDE_CULL = (float)((2.0 * 1.01) * 0.2202504256522561 + 0.01);  // circumradius of 0.429 x 0.1
+static_assert(HALF_SHOULDER > 0.2144f && HALF_SHOULDER < 0.2146f && HALF_DEPTH > 0.0499f && HALF_DEPTH < 0.0501f,
+              "COLLIDE_CULL assumes the 0.429 x 0.1 agent rectangle");
+
 template <int N>
 BB_HD void collide_pair(World<N> &s, int a, int b)
 {
+    {
+        const float dx = s.px[b] - s.px[a], dy = s.py[b] - s.py[a];
+        if (dx * dx + dy * dy > COLLIDE_CULL * COLLIDE_CULL) return;
+    }
     const F3 ca = s.pos(a), fa = forward(s.q(a));
     const F3 ra = f3(fa.y, -fa.x, 0.f);
     const F3 hwa = ra * HALF_SHOULDER, hda = fa * HALF_DEPTH;

@@ -71,11 +71,37 @@ def oracle_flags(per_world_rng=False, tag_mask=True, one_on_one=True):
             | (0 if one_on_one else O.FLAG_FULL_GAME))
 
 
+def sparse_actions(oracle: Oracle, p_act: float = 0.02, seed: int = 5):
+    """actions_fn of a mostly idle offence: agent 0 of every world stands still
+    with probability 1 - p_act, else takes a uniform action over the
+    [2,8,3,2,2,2] buckets; the other agents keep the actions the defence AI
+    wrote (hardCodeDefenseSystem, game.cpp:651-755), so it reaches the
+    offender and tags it (agentCollisionSystem)."""
+    rng = np.random.default_rng(seed)
+    hi = np.array([2, 8, 3, 2, 2, 2])
+
+    def fn(t):
+        a = oracle.export("action").copy()
+        W = a.shape[0]
+        r = (rng.random((W, 6)) * hi).astype(np.int32)
+        r[rng.random(W) >= p_act] = 0
+        a[:, 0] = r
+        return a
+    return fn
+
+
+def count_tags(oracle: Oracle) -> int:
+    """Worlds whose offender was just tagged (-10 / +10 pair, game.cpp:626-629)."""
+    r = oracle.export("reward")
+    return int(((r <= -9.0).any(axis=1) & (r >= 9.0).any(axis=1)).sum())
+
+
 def run_lockstep(sim, oracle: Oracle, steps: int, seed: int = 321, check_every: int = 50,
-                 actions_fn=None, atol: float = FLOAT_ATOL, step0: int = 0):
+                 actions_fn=None, atol: float = FLOAT_ATOL, step0: int = 0, on_step=None):
     """Drive sim and oracle with identical actions; assert parity every
     `check_every` steps and at the end.  actions_fn(t) -> int32 array
-    [W,N,6] or None for the synthetic threefry workload."""
+    [W,N,6] or None for the synthetic threefry workload; on_step(t) is
+    called after each step (e.g. to count events on the oracle)."""
     worst = {}
     for t in range(steps):
         if actions_fn is None:
@@ -88,6 +114,8 @@ def run_lockstep(sim, oracle: Oracle, steps: int, seed: int = 321, check_every: 
                 oracle.set_actions(a)
         sim.step()
         oracle.step()
+        if on_step is not None:
+            on_step(t)
         if (t + 1) % check_every == 0 or t + 1 == steps:
             bad, ident = compare(sim, oracle, atol=atol)
             assert not bad, f"step {t + 1}: {bad}"

@@ -6,7 +6,7 @@ import torch
 
 from madrona_basketball_amd import ExecMode
 from oracle.oracle import Oracle
-from tests.helpers import compare, make_sim, oracle_flags, run_lockstep, sim_np
+from tests.helpers import compare, count_tags, make_sim, oracle_flags, run_lockstep, sim_np, sparse_actions
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -40,6 +40,18 @@ def test_random_rollout(per_world_rng):
     o = Oracle(W, flags=oracle_flags(per_world_rng=per_world_rng))
     worst = run_lockstep(sim, o, 1500, check_every=50)
     assert worst["observations"] == 1.0
+
+
+def test_tag_heavy_rollout():
+    """Mostly idle offenders: the defence AI tags them (SAT contact, -10/+10,
+    delayed reset) -- the contact path random play almost never reaches."""
+    W = 256
+    sim = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    o = Oracle(W, flags=oracle_flags(per_world_rng=True))
+    tags = [0]
+    run_lockstep(sim, o, 800, check_every=20, actions_fn=sparse_actions(o),
+                 on_step=lambda t: tags.__setitem__(0, tags[0] + count_tags(o)))
+    assert tags[0] >= 100, tags[0]
 
 
 @pytest.mark.parametrize("n_agents", [4, 6, 8, 10])

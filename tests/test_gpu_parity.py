@@ -10,7 +10,7 @@ import torch
 
 from madrona_basketball_amd import ExecMode
 from oracle.oracle import Oracle
-from tests.helpers import ALL_COLUMNS, compare, make_sim, oracle_flags, run_lockstep, sim_np
+from tests.helpers import ALL_COLUMNS, compare, count_tags, make_sim, oracle_flags, run_lockstep, sim_np, sparse_actions
 
 pytestmark = pytest.mark.gpu
 
