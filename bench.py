@@ -29,21 +29,37 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(num_agents: int, seconds: float):
-    """The oracle (a single-threaded C restatement of the reference's CPU
-    executor) on a bounded sample of the same workload."""
+def _cpu_worker(job):
+    """One process of the CPU baseline: the oracle (a single-threaded C
+    restatement of the reference's CPU executor) stepping its own worlds."""
+    num_agents, seconds, worlds = job
     from oracle.oracle import Oracle
     from oracle import oracle as O
-    W = 4096
-    o = Oracle(W, num_agents=num_agents, flags=O.FLAG_PER_WORLD_RNG)
+    o = Oracle(worlds, num_agents=num_agents, flags=O.FLAG_PER_WORLD_RNG)
     o.run_random(5, 321, 0)  # warm
     steps, elapsed = 0, 0.0
     while elapsed < seconds:
         elapsed += o.run_random(10, 321, 5 + steps)
         steps += 10
-    return {"value": W * steps / elapsed, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{W} worlds x {steps} steps, {num_agents} agents, threefry random actions, "
-                      f"single thread ({elapsed:.1f} s)"}
+    return worlds, steps, elapsed
+
+
+def cpu_baseline(num_agents: int, seconds: float, procs: int):
+    """The oracle on `procs` host cores (one process each, spawned before this
+    process touches the GPU), each on a bounded sample of the same workload;
+    the rates of the concurrent processes add up."""
+    worlds = 2048
+    if procs <= 1:
+        res = [_cpu_worker((num_agents, seconds, worlds))]
+    else:
+        import multiprocessing as mp
+        with mp.get_context("spawn").Pool(procs) as pool:
+            res = pool.map(_cpu_worker, [(num_agents, seconds, worlds)] * procs)
+    value = sum(w * st / el for w, st, el in res)
+    steps = min(st for _, st, _ in res)
+    return {"value": value, "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} process(es) x {worlds} worlds x >= {steps} steps each, {num_agents} agents, "
+                      f"threefry random actions, ~{seconds:.0f} s per process, rates summed"}
 
 
 def load_traffic(workload_key: str):
@@ -69,15 +85,20 @@ def main():
     ap.add_argument("--seed", type=int, default=321)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
+                    help="host processes for the CPU baseline (the GPU box's share is 16 cores)")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.agents, args.cpu_seconds, args.cpu_procs)  # before any GPU call
 
     import torch
     import torch.distributed as dist
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = args.exec == "cuda"
     if on_gpu:
@@ -183,10 +204,8 @@ def main():
     if not on_gpu:
         out["roofline"] = None
         out["config"]["parallelism"] += " (host executor, gloo)"
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.agents, args.cpu_seconds)
-    elif rank == 0:
-        out["cpu_baseline"] = None
+    if rank == 0:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world_size > 1:

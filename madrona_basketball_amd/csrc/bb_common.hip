@@ -90,9 +90,9 @@ hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t
 #undef CALL
 }
 
-hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode)
+hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode, hipEvent_t ev0, hipEvent_t ev1)
 {
-#define CALL(k) launch_step_t<k>(p, mode, s)
+#define CALL(k) launch_step_t<k>(p, mode, s, ev0, ev1)
     BB_DISPATCH_N(n, CALL)
 #undef CALL
 }

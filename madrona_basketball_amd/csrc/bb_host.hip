@@ -471,10 +471,10 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
             hipError_t e = bb::launch_random_actions(s->n, s->p, action_seed, step0 + (uint32_t)k, st);
             if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
         }
-        if (!ev.empty()) (void)hipEventRecord(ev[2 * k], st);
-        hipError_t e = bb::launch_step(s->n, s->p, st);
+        // kernel_ms: the step kernel's own start/end (hipExtLaunchKernel events)
+        hipError_t e = ev.empty() ? bb::launch_step(s->n, s->p, st)
+                                  : bb::launch_step(s->n, s->p, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
-        if (!ev.empty()) (void)hipEventRecord(ev[2 * k + 1], st);
     }
     if (!ev.empty()) {
         hipError_t e = hipEventSynchronize(ev.back());

@@ -17,6 +17,7 @@
 // Replaces the reference's 19 ParallelFor megakernel nodes + 3 sort nodes per
 // step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include "bb_launch.h"
 #include "bb_sim.h"
 
@@ -441,21 +442,25 @@ __global__ __launch_bounds__(256) void k_init(const Params p)
     init_world<N>(p, w);
 }
 
+// ev0/ev1 (optional): hipExtLaunchKernel records the kernel's own start and
+// end in them (the dispatch packet's timestamps, as rocprofv3 reports them).
 template <int N>
-hipError_t launch_step_t(const Params &p, int mode, hipStream_t s)
+hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
     constexpr int WPB = Lanes<N>::WPB;
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+#define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
-    case MODE_FULL: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_FULL>), grid, block, 0, s, p); break;
-    case MODE_IO: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO>), grid, block, 0, s, p); break;
-    case MODE_IO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_IO_OBS>), grid, block, 0, s, p); break;
-    case MODE_DIRECT_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_DIRECT_OBS>), grid, block, 0, s, p); break;
-    case MODE_NO_OBS: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_NO_OBS>), grid, block, 0, s, p); break;
-    case MODE_SKIP: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_SKIP>), grid, block, 0, s, p); break;
-    case MODE_TRACE: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step<N, MODE_TRACE>), grid, block, 0, s, p); break;
+    case MODE_FULL: BB_LAUNCH(MODE_FULL); break;
+    case MODE_IO: BB_LAUNCH(MODE_IO); break;
+    case MODE_IO_OBS: BB_LAUNCH(MODE_IO_OBS); break;
+    case MODE_DIRECT_OBS: BB_LAUNCH(MODE_DIRECT_OBS); break;
+    case MODE_NO_OBS: BB_LAUNCH(MODE_NO_OBS); break;
+    case MODE_SKIP: BB_LAUNCH(MODE_SKIP); break;
+    case MODE_TRACE: BB_LAUNCH(MODE_TRACE); break;
     default: return hipErrorInvalidValue;
     }
+#undef BB_LAUNCH
     return hipGetLastError();
 }
 
@@ -466,7 +471,7 @@ hipError_t launch_init_t(const Params &p, hipStream_t s)
     return hipGetLastError();
 }
 
-template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t);
+template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template <> int step_grid<BB_N>(int64_t num_worlds) { return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB); }
 

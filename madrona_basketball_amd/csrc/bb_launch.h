@@ -18,12 +18,12 @@ enum StepMode : int {
     MODE_TRACE = 6,       // full, plus per-wave phase clocks into Params::diag_ts
 };
 
-template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s);
+template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
 template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)
 
 #define BB_EXTERN_N(n)                                                                  \
-    extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t);      \
+    extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t); \
     extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);           \
     template <> int step_grid<n>(int64_t);
 BB_EXTERN_N(2)
@@ -33,7 +33,8 @@ BB_EXTERN_N(8)
 BB_EXTERN_N(10)
 #undef BB_EXTERN_N
 
-hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL);
+hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL, hipEvent_t ev0 = nullptr,
+                       hipEvent_t ev1 = nullptr);
 hipError_t launch_init(int n, const Params &p, hipStream_t s);
 int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);

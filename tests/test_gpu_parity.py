@@ -38,6 +38,18 @@ def test_gpu_random_rollout_8192x1000(per_world_rng):
     assert worst["agent_pos"] == 1.0, worst
 
 
+def test_gpu_tag_heavy_rollout():
+    """Contact path (agentCollisionSystem SAT, tags, delayed resets) under a
+    mostly idle offence, 4096 worlds x 800 steps vs the oracle."""
+    W = 4096
+    sim = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    o = Oracle(W, flags=oracle_flags(per_world_rng=True))
+    tags = [0]
+    run_lockstep(sim, o, 800, check_every=100, actions_fn=sparse_actions(o),
+                 on_step=lambda t: tags.__setitem__(0, tags[0] + count_tags(o)))
+    assert tags[0] >= 1000, tags[0]
+
+
 def test_gpu_equals_host_executor_bitwise():
     W = 2048
     g = make_sim(ExecMode.CUDA, W, per_world_rng=True)
