@@ -151,7 +151,14 @@ BB_HD double atan01(double t)
     p = fma_d(p, z, 1.0 / 5.0);
     p = fma_d(p, z, -1.0 / 3.0);
     const double at = fma_d(u * z, p, u);
-    return ATAN_HI[i] + (ATAN_LO[i] + at);
+    // table entry by register selects (a per-lane table load would wait on memory)
+    double hi = ATAN_HI[0], lo = ATAN_LO[0];
+#pragma unroll
+    for (int j = 1; j < 9; j++) {
+        hi = (i == j) ? ATAN_HI[j] : hi;
+        lo = (i == j) ? ATAN_LO[j] : lo;
+    }
+    return hi + (lo + at);
 }
 
 BB_HD double atan_d(double x)

@@ -166,6 +166,25 @@ BB_HD T sel(bool c, const T &a, const T &b)
     }
 }
 
+// A kernel-argument value read as a wave-uniform scalar: a runtime choice
+// between two of them stays a register select instead of becoming a per-lane
+// load from the argument segment (select-of-loads -> load-of-select).
+BB_HD float uni(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, x)));
+#else
+    return x;
+#endif
+}
+BB_HD F3 uni(F3 a) { return f3(uni(a.x), uni(a.y), uni(a.z)); }
+BB_HD Q4 uni(Q4 q)
+{
+    Q4 r;
+    r.w = uni(q.w); r.x = uni(q.x); r.y = uni(q.y); r.z = uni(q.z);
+    return r;
+}
+
 // Value of f(j) for j == i, built from selects (i may be a runtime value --
 // e.g. the lane's agent -- while every array index inside f stays constant).
 template <int N, class F>
@@ -408,8 +427,9 @@ BB_HD float sample_uniform(World<N> &s, Ctx &c, float lo, float hi)
 template <int N>
 BB_HD F3 hoop_pos(const Ctx &c, int h)
 {
-    const float *hp = h == 0 ? c.p->hoop0 : c.p->hoop1;
-    return f3(hp[0], hp[1], hp[2]);
+    const F3 h0 = uni(f3(c.p->hoop0[0], c.p->hoop0[1], c.p->hoop0[2]));
+    const F3 h1 = uni(f3(c.p->hoop1[0], c.p->hoop1[1], c.p->hoop1[2]));
+    return sel(h == 0, h0, h1);
 }
 
 BB_HD F3 vec_to_center(const Ctx &c, F3 p)  // findVectorToCenter, helper.cpp:44-48
@@ -426,7 +446,7 @@ BB_HD Q4 start_orientation_eval(int i)  // gen.cpp:196 / :277
 template <int N>
 BB_HD Q4 start_orientation(const Ctx &c, int i)
 {
-    return c.p->start_q[i % 2];
+    return sel(i % 2 == 0, uni(c.p->start_q[0]), uni(c.p->start_q[1]));
 }
 
 // setupAgentPositions (src/helper.cpp:108-160); returns the ball holder id.
@@ -662,15 +682,15 @@ BB_HD MoveOut move_one(const MoveIn &in, const Params &p)
 {
     MoveOut o;
     o.q = in.q;
-    if (in.rotate != 0) o.q = qmul(in.rotate == 1 ? p.turn_q[0] : p.turn_q[1], in.q);
+    if (in.rotate != 0) o.q = qmul(sel(in.rotate == 1, uni(p.turn_q[0]), uni(p.turn_q[1])), in.q);
     o.vel = in.vel; o.px = in.px; o.py = in.py;
     if (in.can_move == 0) return o;
     const int32_t m = in.angle;
-    float sn = p.mv_sin[0], cs = p.mv_cos[0];
+    float sn = uni(p.mv_sin[0]), cs = uni(p.mv_cos[0]);
     if ((uint32_t)m < 8u) {
 #pragma unroll
         for (int k = 1; k < 8; k++)
-            if (m == k) { sn = p.mv_sin[k]; cs = p.mv_cos[k]; }
+            if (m == k) { sn = uni(p.mv_sin[k]); cs = uni(p.mv_cos[k]); }
     } else {
         bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
     }
