@@ -49,7 +49,7 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False, variant: str | None = None,
-          defines: list[str] | None = None) -> str:
+          defines: list[str] | None = None, extra_flags: list[str] | None = None) -> str:
     """Build the library; a `variant` (diagnostics: A/B timing of compile-time
     alternatives) goes to _variants/<variant>/ with extra -D `defines` and is
     loaded only when MADRONA_BB_LIB points at it."""
@@ -65,8 +65,8 @@ def build(force: bool = False, verbose: bool = False, variant: str | None = None
     cmds = []
     for src, extra, objname in UNITS:
         obj = os.path.join(build_dir, objname)
-        cmds.append([cc, *FLAGS, *extra, *[f"-D{d}" for d in (defines or [])], "-c", os.path.join(CSRC, src),
-                     "-o", obj])
+        cmds.append([cc, *FLAGS, *extra, *[f"-D{d}" for d in (defines or [])], *(extra_flags or []), "-c",
+                     os.path.join(CSRC, src), "-o", obj])
         objs.append(obj)
         if verbose:
             print(" ".join(cmds[-1]), file=sys.stderr)
@@ -88,5 +88,6 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--variant", default=None, help="diagnostic build under _variants/<name>/")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a variant")
+    ap.add_argument("--flag", dest="flags", action="append", default=[], help="extra hipcc flag for a variant")
     a = ap.parse_args()
-    print(build(force=a.force, verbose=True, variant=a.variant, defines=a.defines))
+    print(build(force=a.force, verbose=True, variant=a.variant, defines=a.defines, extra_flags=a.flags))

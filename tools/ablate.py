@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--agents", type=int, default=2)
     ap.add_argument("--iters", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--only", type=int, nargs="*", default=None, help="time only these modes, no trace")
     args = ap.parse_args()
     import torch
     import madrona_basketball_amd as mba
@@ -39,10 +40,11 @@ def main():
     torch.cuda.synchronize()
     B = L.bb_algorithmic_bytes_per_world(args.agents)
     read_q, write_q = 28, (B * 0 + 1256 + 15) // 16
-    res = {m: [] for m in MODES}
+    modes = {m: MODES[m] for m in (args.only if args.only is not None else MODES)}
+    res = {m: [] for m in modes}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for r in range(args.rounds):
-        for m in MODES:
+        for m in modes:
             ms = ctypes.c_float()
             rc = L.bb_diag_time(sim._h, m, args.iters, read_q, write_q, stream, ctypes.byref(ms))
             assert rc == 0, L.bb_last_error()
@@ -53,7 +55,8 @@ def main():
         out[MODES[m]] = {"median_us": med, "min_us": min(v), "algorithmic_GBps": B * args.worlds / (med * 1e-6) / 1e9}
         print(f"{MODES[m]:40s} median {med:8.2f} us  min {min(v):8.2f} us  "
               f"alg {out[MODES[m]]['algorithmic_GBps']:7.0f} GB/s", flush=True)
-    out["trace"] = trace(L, sim, stream)
+    if args.only is None:
+        out["trace"] = trace(L, sim, stream)
     print(json.dumps({"worlds": args.worlds, "agents": args.agents, "results": out}))
 
 
