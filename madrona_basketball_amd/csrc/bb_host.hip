@@ -551,8 +551,10 @@ int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
 int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t write_q, void *stream,
                  float *avg_ms)
 {
-    // MODE_SKIP (5): read_q carries the skip mask (Params::diag_skip)
+    // MODE_SKIP (5): read_q carries the skip mask (Params::diag_skip), write_q
+    // the run-twice mask (Params::diag_dup)
     const uint32_t skip = (mode == 5) ? (uint32_t)read_q : 0u;
+    const uint32_t dup = (mode == 5) ? (uint32_t)write_q : 0u;
     if (!s || s->cfg.exec_mode != BB_EXEC_CUDA || iters < 1 || !avg_ms) return fail(BB_ERR_INVALID_ARG, "bb_diag_time");
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;
@@ -568,6 +570,8 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
     (void)hipEventCreate(&e1);
     bb::Params pp = s->p;
     pp.diag_skip = skip;
+    pp.diag_dup = dup;
+    pp.diag_keep = 0;
     auto once = [&]() -> hipError_t {
         if (mode == 100) return bb::launch_stream_probe(src, dst, W, read_q, write_q, st);
         return bb::launch_step(s->n, pp, st, mode);

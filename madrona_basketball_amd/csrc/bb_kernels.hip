@@ -54,9 +54,14 @@ struct Lanes {
 
 // Row tile of the agent-lane kernel: the row is emitted in PH passes of QP
 // float4 pieces so the tile stays ~16 KB (>= 8 waves per CU).
+#ifndef BB_OBS_WRITE_ALIGN
+#define BB_OBS_WRITE_ALIGN 16  // bytes: row writes end on this boundary (zero pieces added)
+#endif
 template <int N>
 struct PhasedTile {
-    static constexpr int QW = (obs_used(N) + 3) / 4;
+    static constexpr int QU = (obs_used(N) + 3) / 4;  // pieces holding row values
+    static constexpr int QA = (QU * 16 + BB_OBS_WRITE_ALIGN - 1) / BB_OBS_WRITE_ALIGN * BB_OBS_WRITE_ALIGN / 16;
+    static constexpr int QW = QA < obs_width(N) / 4 ? QA : obs_width(N) / 4;  // pieces written
     static constexpr int PH = (QW + 14) / 15;
     static constexpr int QP = (QW + PH - 1) / PH;
     static constexpr int RS = QP * 4 + (QP % 2 == 0 ? 4 : 0);  // == 4 mod 8 dwords
@@ -194,9 +199,10 @@ struct LaneAgents {
 // its stores, addresses are 32-bit offsets from the wave's first row.
 typedef float vf4 __attribute__((ext_vector_type(4)));  // plain 16-byte loads/stores
 
-template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL>
+template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL, int QZ>
 __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64_t staged, int lane)
 {
+    // pieces q >= QZ of this pass are zeros (row padding), not read from the tile
     constexpr int OW = obs_width(N);
     constexpr int DR = WAVE / QT, DQ = WAVE % QT;  // advance of f by 64
     constexpr int BS = QT <= 16 ? QT : (QT + 1) / 2;
@@ -211,7 +217,10 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
             if (b0 + j < QT) {
                 ok[j] = (QN == QT || q < QN) && (ALL || ((staged >> r) & 1ull));
                 go[j] = (uint32_t)(r * (RSTR * OW * 4) + q * 16);
-                if (ok[j]) v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
+                if (ok[j]) {
+                    v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
+                    if (QZ < QN && q >= QZ) v[j] = vf4{0.f, 0.f, 0.f, 0.f};
+                }
                 r += DR;
                 q += DQ;
                 if (q >= QT) { q -= QT; r += 1; }
@@ -223,12 +232,12 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
     }
 }
 
-template <int N, int QT, int RS, int Q0, int QN, int RSTR>
+template <int N, int QT, int RS, int Q0, int QN, int RSTR, int QZ = QN>
 __device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane)
 {
     char *base = (char *)(obs + row0 * obs_width(N) + 4 * Q0);  // wave-uniform
-    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true>(tile, base, staged, lane);
-    else flush_rows<N, QT, RS, Q0, QN, RSTR, false>(tile, base, staged, lane);
+    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true, QZ>(tile, base, staged, lane);
+    else flush_rows<N, QT, RS, Q0, QN, RSTR, false, QZ>(tile, base, staged, lane);
 }
 
 struct Intrinsic {
@@ -256,7 +265,8 @@ __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, cons
     if (fast) emit_phase<N, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     __syncthreads();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
-    flush_tile<N, T::QP, T::RS, Q0, QN, 1>(tile, c.p->c.obs, row0, __ballot(fast), lane);
+    constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ>(tile, c.p->c.obs, row0, __ballot(fast), lane);
     if constexpr (PHASE + 1 < T::PH) {
         __syncthreads();
         obs_phases<N, MODE, PHASE + 1>(v, c, sh, share, fast, tile, row0, lane, ib);
@@ -281,7 +291,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 0);
     if (active) {
         load_world(s, p, w);
-        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip);
+        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
     }
     trace_point<MODE>(p, 7);
@@ -360,7 +370,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 0);
     if (active) {
         load_world(s, p, w);
-        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, EachAgent(), p.diag_skip);
+        if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, EachAgent(), p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
     trace_point<MODE>(p, 7);

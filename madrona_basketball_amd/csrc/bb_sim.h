@@ -261,6 +261,8 @@ struct Params {
     float rot_thresh;            // (float)acos(c) > pi/8  <=>  c < rot_thresh   game.cpp:746-747
     int32_t rot_exact;           // 1: threshold not verified, evaluate acos
     uint32_t diag_skip;          // diagnostics only (MODE_SKIP): systems to leave out
+    uint32_t diag_dup;           // diagnostics only (MODE_SKIP): systems to run twice
+    uint32_t diag_keep;          // diagnostics only: 0 (the duplicate run's result is dropped)
     uint64_t *diag_ts;           // diagnostics only (MODE_TRACE): TRACE_POINTS clocks per wave
 };
 
@@ -1553,14 +1555,26 @@ BB_HD void sys_fill_obs(const World<N> &s, const Ctx &c)
 }
 
 // ------------------------------------------------------------------ one step
-// Systems 1-17 (everything before fillObservations).  `skip` leaves out the
-// systems whose bit (1 << system number) is set -- timing attribution only
-// (bb_diag_time); the game passes 0 and the tests fold away.
+// Systems 1-17 (everything before fillObservations).  Timing attribution
+// only (bb_diag_time): `skip` leaves out the systems whose bit (1 << system
+// number) is set; `dup` runs them a second time on a copy of the world whose
+// result is dropped (c.p->diag_keep is 0 at run time), so the added time is
+// the system's own cost on the unchanged trajectory.  The game passes 0 for
+// both and the tests fold away.
 template <int N, class A = EachAgent>
-BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t skip = 0)
+BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t skip = 0, uint32_t dup = 0)
 {
     const uint32_t flags = c.p->flags;
-#define BB_RUN(bit, stmt) if (!(skip & (1u << (bit)))) { stmt; }
+#define BB_RUN(bit, stmt)                                                   \
+    if (!(skip & (1u << (bit)))) { stmt; }                                  \
+    if (dup & (1u << (bit))) {                                              \
+        World<N> s_dup = s;                                                 \
+        {                                                                   \
+            World<N> &s = s_dup;                                            \
+            stmt;                                                           \
+        }                                                                   \
+        if (c.p->diag_keep) s = s_dup;                                      \
+    }
     ag.mark(1);
     BB_RUN(1, sys_tick(s))
     BB_RUN(2, sys_action_mask(s, flags))

@@ -1,5 +1,8 @@
-"""Per-system time attribution: full kernel minus one system at a time
-(MODE_SKIP; the skipped system's state effects are lost, timing only)."""
+"""Per-system time attribution (MODE_SKIP variants of k_step, timing only):
+  skip: the kernel without one system (its state effects are lost, so later
+        systems see a different trajectory -- confounded);
+  dup:  the kernel with one system run a second time on a copy whose result
+        is dropped (same trajectory; the added time is the system's cost)."""
 import argparse, ctypes, os, statistics, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -26,12 +29,12 @@ def main():
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     snap = sim.snapshot()
 
-    def t(mode, skip=0):
+    def t(mode, skip=0, dup=0):
         v = []
         for _ in range(a.rounds):
             sim.restore(snap)
             ms = ctypes.c_float()
-            assert L.bb_diag_time(sim._h, mode, a.iters, skip, 0, st, ctypes.byref(ms)) == 0, L.bb_last_error()
+            assert L.bb_diag_time(sim._h, mode, a.iters, skip, dup, st, ctypes.byref(ms)) == 0, L.bb_last_error()
             v.append(ms.value * 1e3)
         return statistics.median(v)
     base = t(5)  # MODE_SKIP with empty mask == full
@@ -42,6 +45,11 @@ def main():
         print(f"  without {n:12s} {x:8.2f} us   saves {base - x:6.2f} us")
     allsys = t(5, sum(1 << b for b in NAMES))
     print(f"  without all systems {allsys:.2f} us")
+    for b, n in NAMES.items():
+        x = t(5, 0, 1 << b)
+        print(f"  twice   {n:12s} {x:8.2f} us   adds  {x - base:6.2f} us")
+    x = t(5, 0, sum(1 << b for b in NAMES))
+    print(f"  all systems twice {x:.2f} us   adds {x - base:.2f} us")
 
 
 if __name__ == "__main__":

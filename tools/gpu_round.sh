@@ -62,6 +62,13 @@ for s in $STEPS; do
             --output-format csv -- python3 "$ROOT/bench.py" --steps 50 --warmup 5 --no-cpu-baseline ) || exit $?
         python3 tools/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" W65536_N2 --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
         ;;
+    pmcv:*) v=${s#pmcv:}
+        for c in FETCH_SIZE WRITE_SIZE; do
+            ( cd /tmp && export TMPDIR=/tmp && \
+              MADRONA_BB_LIB=$ROOT/madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so \
+              run "pmc_${v}_$c" 300 rocprofv3 --pmc $c -d "$OUT/pmc_${v}_$c" -o run --output-format csv -- \
+                python3 "$ROOT/tools/ablate.py" --worlds 65536 --iters 20 --rounds 1 --only 0 ) || exit $?
+        done ;;
     ab:*) v=${s#ab:}
         MADRONA_BB_LIB=$ROOT/madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so \
             run "ablate_$v" 600 python tools/ablate.py --worlds 65536 ;;
