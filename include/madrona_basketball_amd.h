@@ -12,6 +12,9 @@
  *   bb_step             <- Manager::step               src/mgr.cpp:243-246
  *   bb_step_n           <- n x Manager::step (+ optional on-device random
  *                          actions, the bench workload of scripts/run.py:6-19)
+ *   bb_step_n_staged    <- n x (actions[:] = a_k; Manager::step), the
+ *                          scripts/run.py:10-15 loop with a_k staged in HBM
+ *   bb_fill_random_actions <- (new) stages a_k for bb_step_n_staged
  *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
  *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
  *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
@@ -144,6 +147,19 @@ int bb_step_n(bb_sim *sim, int32_t n, int32_t random_actions, uint32_t action_se
 /* Only the synthetic action write (the bench's stand-in for the Python
  * `actions[:] = ...` write of scripts/env.py:147). */
 int bb_write_random_actions(bb_sim *sim, uint32_t action_seed, uint32_t step, void *stream);
+
+/* n steps whose actions are already resident: step k reads its actions from
+ * (and the defence AI writes its overrides back to) the int32 rows
+ * actions + k * num_worlds * num_agents * 6 (layout [n][W][N][6], memory of the
+ * simulator's device in CUDA mode, host memory in CPU mode) instead of the
+ * action tensor; afterwards the action tensor holds step n-1's rows.
+ * kernel_ms as in bb_step_n. */
+int bb_step_n_staged(bb_sim *sim, int32_t n, int32_t *actions, void *stream, float *kernel_ms);
+
+/* Stage n steps of the synthetic workload of bb_step_n (steps step0..step0+n-1)
+ * into actions[n][W][N][6] for bb_step_n_staged. */
+int bb_fill_random_actions(bb_sim *sim, int32_t *actions, int32_t n, uint32_t action_seed, uint32_t step0,
+                           void *stream);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

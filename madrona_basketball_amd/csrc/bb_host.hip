@@ -491,6 +491,77 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
     return BB_OK;
 }
 
+int bb_fill_random_actions(bb_sim *s, int32_t *actions, int32_t n, uint32_t action_seed, uint32_t step0,
+                           void *stream)
+{
+    if (!s || (!actions && n > 0) || n < 0) return fail(BB_ERR_INVALID_ARG, "bb_fill_random_actions");
+    const int64_t rows = s->cfg.num_worlds * s->n * 6;
+    bb::Params pp = s->p;
+    for (int32_t k = 0; k < n; k++) {
+        pp.c.action = actions + (int64_t)k * rows;
+        if (s->cfg.exec_mode == BB_EXEC_CUDA) {
+            DeviceGuard g(s->device);
+            hipError_t e = bb::launch_random_actions(s->n, pp, action_seed, step0 + (uint32_t)k, (hipStream_t)stream);
+            if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
+        } else {
+            int rc = bb::host_random_actions(s->n, pp, action_seed, step0 + (uint32_t)k);
+            if (rc != BB_OK) return rc;
+        }
+    }
+    return BB_OK;
+}
+
+int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float *kernel_ms)
+{
+    if (!s || n < 0 || (!actions && n > 0)) return fail(BB_ERR_INVALID_ARG, "bb_step_n_staged");
+    const int64_t rows = s->cfg.num_worlds * s->n * 6;
+    bb::Params pp = s->p;
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) {
+        for (int32_t k = 0; k < n; k++) {
+            pp.c.action = actions + (int64_t)k * rows;
+            int rc = bb::host_step(s->n, pp, host_threads_for(s->cfg.num_worlds));
+            if (rc != BB_OK) return rc;
+        }
+        if (n > 0) std::memcpy(s->p.c.action, actions + (int64_t)(n - 1) * rows, (size_t)rows * 4);
+        if (kernel_ms) *kernel_ms = 0.f;
+        return BB_OK;
+    }
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    std::vector<hipEvent_t> ev;
+    if (kernel_ms && n > 0) {
+        ev.resize((size_t)2 * n);
+        for (auto &e : ev) {
+            hipError_t he = hipEventCreate(&e);
+            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
+        }
+    }
+    for (int32_t k = 0; k < n; k++) {
+        pp.c.action = actions + (int64_t)k * rows;
+        hipError_t e = ev.empty() ? bb::launch_step(s->n, pp, st)
+                                  : bb::launch_step(s->n, pp, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
+        if (e != hipSuccess) return hip_fail(e, "launch step kernel");
+    }
+    if (n > 0) {
+        hipError_t e = hipMemcpyAsync(s->p.c.action, actions + (int64_t)(n - 1) * rows, (size_t)rows * 4,
+                                      hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return hip_fail(e, "copy last actions");
+    }
+    if (!ev.empty()) {
+        hipError_t e = hipEventSynchronize(ev.back());
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        double total = 0.0;
+        for (int32_t k = 0; k < n; k++) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+            total += ms;
+        }
+        for (auto &x : ev) (void)hipEventDestroy(x);
+        *kernel_ms = (float)total;
+    }
+    return BB_OK;
+}
+
 int bb_set_action(bb_sim *s, int32_t world_idx, int32_t agent_idx, int32_t move_speed, int32_t move_angle,
                   int32_t rotate, int32_t grab, int32_t pass, int32_t shoot, void *stream)
 {

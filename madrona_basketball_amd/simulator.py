@@ -192,6 +192,30 @@ class SimpleGridworldSimulator:
                                          ctypes.byref(ms) if time_kernels else None), "step_n")
         return ms.value if time_kernels else None
 
+    def stage_random_actions(self, n: int, action_seed: int = 321, step0: int = 0) -> torch.Tensor:
+        """[n, W, N, 6] int32 tensor (on the sim's device) holding the synthetic
+        workload of step_n(random_actions=True) for steps step0..step0+n-1."""
+        buf = torch.empty((n, self._num_worlds, self._num_agents, 6), dtype=torch.int32, device=self._device)
+        _lib.check(_lib.load().bb_fill_random_actions(self._h, ctypes.c_void_p(buf.data_ptr()), int(n),
+                                                      int(action_seed) & 0xFFFFFFFF, int(step0) & 0xFFFFFFFF,
+                                                      self._stream()), "fill_random_actions")
+        return buf
+
+    def step_n_staged(self, actions: torch.Tensor, time_kernels: bool = False):
+        """len(actions) steps, step k reading actions[k] ([W, N, 6] int32, on the
+        sim's device) in place of the action tensor (the defence AI's
+        overrides are written back into actions[k]); returns summed
+        step-kernel ms when time_kernels (CUDA mode)."""
+        n = actions.shape[0]
+        if (tuple(actions.shape[1:]) != (self._num_worlds, self._num_agents, 6) or actions.dtype != torch.int32
+                or not actions.is_contiguous() or actions.device != self._device):
+            raise ValueError("actions must be a contiguous int32 [n, num_worlds, num_agents, 6] tensor "
+                             "on the simulator's device")
+        ms = ctypes.c_float(0.0)
+        _lib.check(_lib.load().bb_step_n_staged(self._h, int(n), ctypes.c_void_p(actions.data_ptr()), self._stream(),
+                                                ctypes.byref(ms) if time_kernels else None), "step_n_staged")
+        return ms.value if time_kernels else None
+
     def write_random_actions(self, action_seed: int, step: int) -> None:
         _lib.check(_lib.load().bb_write_random_actions(self._h, int(action_seed) & 0xFFFFFFFF,
                                                        int(step) & 0xFFFFFFFF, self._stream()),

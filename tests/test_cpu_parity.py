@@ -42,6 +42,20 @@ def test_random_rollout(per_world_rng):
     assert worst["observations"] == 1.0
 
 
+def test_staged_actions_equal_per_step_writes():
+    """bb_step_n_staged (actions resident in a [n,W,N,6] buffer, the bench
+    path) == bb_step_n with the same synthetic actions written before each
+    step, on every column."""
+    W, n = 128, 300
+    a = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    b = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    a.step_n(n, random_actions=True, action_seed=321, step0=7)
+    staged = b.stage_random_actions(n, action_seed=321, step0=7)
+    b.step_n_staged(staged)
+    for name in a._views:
+        assert torch.equal(a._views[name], b._views[name]), name
+
+
 def test_tag_heavy_rollout():
     """Mostly idle offenders: the defence AI tags them (SAT contact, -10/+10,
     delayed reset) -- the contact path random play almost never reaches."""

@@ -38,6 +38,23 @@ def test_gpu_random_rollout_8192x1000(per_world_rng):
     assert worst["agent_pos"] == 1.0, worst
 
 
+def test_gpu_staged_actions_equal_per_step_writes():
+    """The bench path (actions staged in HBM, bb_step_n_staged) == per-step
+    action writes + step, bit for bit, and == the host executor."""
+    W, n = 8192, 200
+    a = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    b = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    h = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    a.step_n(n, random_actions=True, action_seed=321, step0=3)
+    staged = b.stage_random_actions(n, action_seed=321, step0=3)
+    b.step_n_staged(staged)
+    h.step_n(n, random_actions=True, action_seed=321, step0=3)
+    torch.cuda.synchronize()
+    for name in a._views:
+        assert torch.equal(a._views[name], b._views[name]), name
+        assert torch.equal(a._views[name].cpu(), h._views[name]), name
+
+
 def test_gpu_tag_heavy_rollout():
     """Contact path (agentCollisionSystem SAT, tags, delayed resets) under a
     mostly idle offence, 4096 worlds x 800 steps vs the oracle."""
