@@ -273,6 +273,12 @@ __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, cons
     }
 }
 
+struct LaneOrig {
+    WorldOrig world;
+    OrigAgent agent;
+};
+static_assert(sizeof(LaneOrig) <= 4 * 52, "fits a row of the observation tile");
+
 // One lane per agent: lane = (w - w0) * N + k.
 template <int N, int MODE>
 __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
@@ -289,8 +295,20 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;  // the world with this lane's agent in slot 0
     trace_point<MODE>(p, 0);
+    // The event-only words as loaded (store only on change, see Orig) wait
+    // in the lane's row of the observation tile, which is free until the
+    // observation pass: registers stay with the systems.
+    LaneOrig *lo = (LaneOrig *)(tile + lane * PhasedTile<N>::RS);
     if (active) {
         load_world(s, p, w);
+        {
+            Orig<N> o;
+            capture(o, s);
+            LaneOrig x;
+            x.world = world_orig(o);
+            x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
+            *lo = x;
+        }
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
     }
@@ -301,8 +319,13 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         // reward + state columns first, so their stores drain while the
         // observation row is built
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
-        store_world_agent(v, p, w * N + k, 0);
-        if (k == 0) store_world_shared(s, p, w);
+        const LaneOrig x = *lo;
+        store_world_agent(v, p, w * N + k, 0, &x.agent);
+        if (k == 0) {
+            Orig<N> o;
+            set_world_orig(o, x.world);
+            store_world_shared(s, p, w, &o);
+        }
     }
     trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
@@ -368,8 +391,10 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
     World<N> s;
     Ctx c = make_ctx(p, w, true);
     trace_point<MODE>(p, 0);
+    Orig<N> o;  // event-only words as loaded (store only on change)
     if (active) {
         load_world(s, p, w);
+        capture(o, s);
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, EachAgent(), p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c);
     }
@@ -379,7 +404,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
         // reward + state columns first, so their stores drain while the
         // observation rows are built
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward(s);
-        store_world(s, p, w);
+        store_world(s, p, w, &o);
     }
     trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) {

@@ -1729,31 +1729,115 @@ BB_HD void load_world(World<N> &s, const Params &p, int64_t w)
     }
 }
 
-// World-level columns (GameState, WorldClock, RNG counter, ball).
+// Event-only words (SURVEY.md 8(d) leaves them out of the per-step traffic):
+// GameState except the two clocks, BallPhysics, Grabbed, WorldClock, the RNG
+// counter; per agent Reset, Inbounding and the constant attributes (0-4, 9).
+// Snapshotted right after the load, they let the store phase rewrite such a
+// column only when the step changed it -- memory still holds the loaded
+// words, so skipping the store is exact.
+struct OrigAgent {
+    int32_t rst, inb, allow;
+    uint32_t attr[6];  // attributes 0-4, 9
+};
+struct WorldOrig {
+    uint32_t game[14];
+    uint32_t phys[7], grab[2], clock, rng;
+};
 template <int N>
-BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w)
+struct Orig : WorldOrig {
+    OrigAgent ag[N];
+};
+template <int N>
+BB_HD WorldOrig world_orig(const Orig<N> &o) { return o; }
+template <int N>
+BB_HD void set_world_orig(Orig<N> &o, const WorldOrig &w) { (WorldOrig &)o = w; }
+
+template <int N>
+BB_HD void game_words(const World<N> &s, uint32_t (&g)[14])
+{
+    g[0] = (uint32_t)s.g_inb; g[1] = (uint32_t)s.g_live; g[2] = fbits(s.g_period); g[3] = fbits(s.g_poss);
+    g[4] = (uint32_t)s.g_h0; g[5] = fbits(s.g_s0); g[6] = (uint32_t)s.g_h1; g[7] = fbits(s.g_s1);
+    g[8] = fbits(s.g_clock); g[9] = fbits(s.g_shot); g[10] = fbits(s.g_bask); g[11] = fbits(s.g_oob);
+    g[12] = fbits(s.g_inbclk); g[13] = (uint32_t)s.g_1v1;
+}
+template <int N>
+BB_HD void phys_words(const World<N> &s, uint32_t (&ph)[7])
+{
+    ph[0] = (uint32_t)s.fl; ph[1] = (uint32_t)s.lta; ph[2] = (uint32_t)s.ltt; ph[3] = (uint32_t)s.sba;
+    ph[4] = (uint32_t)s.sbt; ph[5] = (uint32_t)s.spv; ph[6] = (uint32_t)s.gin;
+}
+template <int N>
+BB_HD OrigAgent orig_agent(const World<N> &s, int i)
+{
+    OrigAgent o;
+    o.rst = s.rst[i]; o.inb = s.inb[i]; o.allow = s.allow[i];
+#pragma unroll
+    for (int k = 0; k < 5; k++) o.attr[k] = fbits(s.attr[i][k]);
+    o.attr[5] = fbits(s.attr[i][9]);
+    return o;
+}
+template <int N>
+BB_HD void capture(Orig<N> &o, const World<N> &s)
+{
+    game_words(s, o.game);
+    phys_words(s, o.phys);
+    o.grab[0] = (uint32_t)s.grab; o.grab[1] = (uint32_t)s.holder;
+    o.clock = (uint32_t)s.reset_now; o.rng = s.rng_ctr;
+#pragma unroll
+    for (int i = 0; i < N; i++) o.ag[i] = orig_agent(s, i);
+}
+
+template <int NW>
+BB_HD bool differ(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
+{
+    bool d = false;
+#pragma unroll
+    for (int k = 0; k < NW; k++) d |= a[k] != b[k];
+    return d;
+}
+
+// World-level columns (GameState, WorldClock, RNG counter, ball).  With `o`,
+// the event-only words are rewritten only when changed (see Orig).
+template <int N>
+BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, const Orig<N> *o = nullptr)
 {
     const Columns &c = p.c;
-    const uint32_t g[14] = {(uint32_t)s.g_inb, (uint32_t)s.g_live, fbits(s.g_period), fbits(s.g_poss),
-                            (uint32_t)s.g_h0, fbits(s.g_s0), (uint32_t)s.g_h1, fbits(s.g_s1),
-                            fbits(s.g_clock), fbits(s.g_shot), fbits(s.g_bask), fbits(s.g_oob),
-                            fbits(s.g_inbclk), (uint32_t)s.g_1v1};
-    store_words<14>(c.game_state, w, g);
-    c.world_clock[w] = s.reset_now;
-    c.rng_counter[w] = s.rng_ctr;
+    uint32_t g[14];
+    game_words(s, g);
+    bool game_ev = o == nullptr;
+    if (o) {
+#pragma unroll
+        for (int k = 0; k < 14; k++)
+            if (k != 8 && k != 9) game_ev |= g[k] != o->game[k];
+    }
+    if (game_ev) {
+        store_words<14>(c.game_state, w, g);
+    } else {  // game and shot clock only
+        const uint32_t clk[2] = {g[8], g[9]};
+        store_words<2>(c.game_state + w * 14 + 8, 0, clk);
+    }
+    if (!o || (uint32_t)s.reset_now != o->clock) c.world_clock[w] = s.reset_now;
+    if (!o || s.rng_ctr != o->rng) c.rng_counter[w] = s.rng_ctr;
     float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
     bp[0] = s.bx; bp[1] = s.by; bp[2] = s.bz;
     bv[0] = s.bvx; bv[1] = s.bvy; bv[2] = s.bvz;
-    int32_t *ph = c.ball_physics + w * 7;
-    ph[0] = s.fl; ph[1] = s.lta; ph[2] = s.ltt; ph[3] = s.sba; ph[4] = s.sbt; ph[5] = s.spv; ph[6] = s.gin;
+    uint32_t ph[7];
+    phys_words(s, ph);
+    if (!o || differ(ph, o->phys)) {
+        uint32_t *d = (uint32_t *)c.ball_physics + w * 7;
+#pragma unroll
+        for (int k = 0; k < 7; k++) d[k] = ph[k];
+    }
     const uint32_t gb[2] = {(uint32_t)s.grab, (uint32_t)s.holder};
-    store_words<2>(c.ball_grabbed, w, gb);
+    if (!o || differ(gb, o->grab)) store_words<2>(c.ball_grabbed, w, gb);
 }
 
 // Per-agent columns of agent i (row w*N + i of every [W][N][...] column).
-// Team changes only inside generate/reset, which write it directly.
+// Team changes only inside generate/reset, which write it directly.  With
+// `o` (agent i's event-only words as loaded) those are rewritten only when
+// changed.
 template <int N>
-BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int i)
+BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int i, const OrigAgent *o = nullptr)
 {
     const Columns &c = p.c;
     uint32_t a[6], m[4], pos[3], ps[3], q[4], v[3], ib[2], at[10];
@@ -1768,7 +1852,7 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
     ib[0] = (uint32_t)s.inb[i]; ib[1] = (uint32_t)s.allow[i];
 #pragma unroll
     for (int k = 0; k < 10; k++) at[k] = fbits(s.attr[i][k]);
-    c.reset[r] = s.rst[i];
+    if (!o || s.rst[i] != o->rst) c.reset[r] = s.rst[i];
     store_words<6>(c.action, r, a);
     store_words<4>(c.action_mask, r, m);
     store_words<3>(c.agent_pos, r, pos);
@@ -1779,16 +1863,28 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
     store_words<3>(c.agent_vel, r, v);
     c.cooldown[r] = s.cd[i];
     c.cur_step[r] = s.step[i];
-    store_words<2>(c.inbounding, r, ib);
-    store_words<10>(c.attributes, r, at);
+    if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2>(c.inbounding, r, ib);
+    bool attr_ev = o == nullptr;
+    if (o) {
+#pragma unroll
+        for (int k = 0; k < 5; k++) attr_ev |= at[k] != o->attr[k];
+        attr_ev |= at[9] != o->attr[5];
+    }
+    if (attr_ev) {
+        store_words<10>(c.attributes, r, at);
+    } else {  // target position (5-7) and shot percentage (8)
+        uint32_t *d = (uint32_t *)c.attributes + r * 10 + 5;
+#pragma unroll
+        for (int k = 0; k < 4; k++) d[k] = at[5 + k];
+    }
 }
 
 template <int N>
-BB_HD void store_world(const World<N> &s, const Params &p, int64_t w)
+BB_HD void store_world(const World<N> &s, const Params &p, int64_t w, const Orig<N> *o = nullptr)
 {
-    store_world_shared(s, p, w);
+    store_world_shared(s, p, w, o);
 #pragma unroll
-    for (int i = 0; i < N; i++) store_world_agent(s, p, w * N + i, i);
+    for (int i = 0; i < N; i++) store_world_agent(s, p, w * N + i, i, o ? &o->ag[i] : nullptr);
 }
 
 // Constant columns written once at construction: entity ids, hoop positions.
@@ -1821,9 +1917,11 @@ BB_HD void step_one_world(const Params &p, int64_t w)
 {
     World<N> s;
     load_world(s, p, w);
+    Orig<N> o;
+    capture(o, s);
     Ctx c = make_ctx(p, w);
     step_world(s, c);
-    store_world(s, p, w);
+    store_world(s, p, w, &o);
 }
 
 }  // namespace bb
