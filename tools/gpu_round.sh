@@ -43,10 +43,10 @@ for s in $STEPS; do
     smoke) run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rA ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 100 ;;
-    bench262k) run bench262k 600 python bench.py --worlds 262144 --steps 500 --warmup 50 --no-cpu-baseline ;;
+    bench262k) run bench262k 600 python bench.py --worlds 262144 --steps 300 --warmup 50 --no-cpu-baseline ;;
     bench8k) run bench8k 600 python bench.py --worlds 8192 --steps 1000 --warmup 100 --no-cpu-baseline ;;
-    bench4) run bench4 600 python bench.py --agents 4 --steps 500 --warmup 50 --no-cpu-baseline ;;
-    bench10) run bench10 600 python bench.py --agents 10 --steps 200 --warmup 20 --no-cpu-baseline ;;
+    bench4) run bench4 600 python bench.py --agents 4 --steps 300 --warmup 50 --no-cpu-baseline ;;
+    bench10) run bench10 600 python bench.py --agents 10 --steps 100 --warmup 20 --no-cpu-baseline ;;
     ablate) run ablate 600 python tools/ablate.py --worlds 65536 ;;
     ablate262k) run ablate262k 600 python tools/ablate.py --worlds 262144 --iters 50 ;;
     systems) run systems 600 python tools/ablate_systems.py --worlds 65536 ;;
