@@ -46,9 +46,14 @@ struct ObsTile {
 #ifndef BB_AGENT_LANES
 #define BB_AGENT_LANES 1
 #endif
+#ifndef BB_LDS_MIN_N
+#define BB_LDS_MIN_N 4  // from this agent count on, the world state lives in LDS
+#endif
 template <int N>
 struct Lanes {
-    static constexpr int LPW = (BB_AGENT_LANES && (N == 2 || N == 4)) ? N : 1;
+    // SHARED: one lane per agent, the world's state in LDS shared by its N lanes
+    static constexpr bool SHARED = N >= BB_LDS_MIN_N;
+    static constexpr int LPW = SHARED ? N : ((BB_AGENT_LANES && (N == 2 || N == 4)) ? N : 1);
     static constexpr int WPB = WAVE / LPW;  // worlds per 64-lane workgroup
 };
 
@@ -378,6 +383,158 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 9);
 }
 
+// ------------------------------------------------------------------ N >= 4
+// One lane per agent; the world's state lives in LDS and its N lanes run the
+// world-level systems on it together (same instructions, same values); the
+// per-agent systems are computed by the agent's lane and exchanged through
+// an LDS buffer (LdsAgents).  No per-lane copy of the world: nothing to spill.
+constexpr int XW = 32;  // words per lane in the exchange buffer (>= Intrinsic)
+
+template <int N, int MODE>
+struct LdsAgents {
+    int k, slot;
+    uint32_t (*x)[XW];
+    const Params *p;
+    template <class T, int NN, class F>
+    __device__ void all(F f, T (&out)[NN]) const
+    {
+        static_assert(NN == N && sizeof(T) <= XW * 4, "exchange slot");
+        const T mine = f(k);
+        __syncthreads();  // earlier readers of the buffer are done
+        __builtin_memcpy(x[slot * N + k], &mine, sizeof(T));
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < N; j++) __builtin_memcpy(&out[j], x[slot * N + j], sizeof(T));
+    }
+    __device__ void mark(int point) const { trace_point<MODE>(*p, point); }
+};
+
+template <int N>
+struct SharedLds {
+    static constexpr int WPW = WAVE / N;  // worlds per wave
+    World<N> world[WPW];
+    uint32_t x[WAVE][XW];
+};
+
+template <int N, int MODE, int PHASE = 0>
+__device__ __forceinline__ void obs_phases_view(const World<N> &s, const Ctx &c, int k, const uint32_t (*x)[XW],
+                                                int slot, bool share, bool fast, float *tile, int64_t row0,
+                                                int lane, int32_t ib)
+{
+    using T = PhasedTile<N>;
+    if (fast) {
+        constexpr int LO = PHASE * T::QP * 4, HI = LO + T::QP * 4;
+        WindowSink<LO, HI> o;
+        o.row = tile + lane * T::RS; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+        auto intr = [&](int j, int q) { return bitsf(x[slot * N + j][q]); };
+        emit_row_view(s, c, k, intr, share, o, ib);
+    }
+    __syncthreads();
+    constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
+    constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ>(tile, c.p->c.obs, row0, __ballot(fast), lane);
+    if constexpr (PHASE + 1 < T::PH) {
+        __syncthreads();
+        obs_phases_view<N, MODE, PHASE + 1>(s, c, k, x, slot, share, fast, tile, row0, lane, ib);
+    }
+}
+
+template <int N, int MODE>
+__device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm)
+{
+    constexpr int WPW = SharedLds<N>::WPW, OW = obs_width(N);
+    const int lane = threadIdx.x;
+    // lanes past WPW*N mirror agents of the last world: they run its systems
+    // (identical LDS writes) but own no row and store nothing
+    const bool lane_used = lane < WPW * N;
+    const int slot = lane_used ? lane / N : WPW - 1;
+    const int k = lane_used ? lane % N : (lane - WPW * N) % N;
+    const int64_t w0 = (int64_t)blockIdx.x * WPW;
+    const int64_t w = w0 + slot;
+    const bool world_ok = w < p.num_worlds;  // uniform over the world's lanes
+    const bool active = lane_used && world_ok;
+    World<N> &s = sm.world[slot];
+    const LdsAgents<N, MODE> ag{k, slot, sm.x, &p};
+    Ctx c = make_ctx(p, w, active && k == 0);
+    trace_point<MODE>(p, 0);
+
+    if (active) {
+        load_world_agent(s, p, w, k);
+        if (k == 0) load_world_shared(s, p, w);
+    }
+    __syncthreads();
+    // event-only words as loaded, parked in the lane's tile row
+    LaneOrig *lo = (LaneOrig *)(tile + lane * PhasedTile<N>::RS);
+    if (active) {
+        Orig<N> o;
+        game_words(s, o.game);
+        phys_words(s, o.phys);
+        o.grab[0] = (uint32_t)s.grab; o.grab[1] = (uint32_t)s.holder;
+        o.clock = (uint32_t)s.reset_now; o.rng = s.rng_ctr;
+        LaneOrig x;
+        x.world = world_orig(o);
+        x.agent = orig_agent(s, k);
+        *lo = x;
+    }
+    if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, 0u);
+    else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
+    __syncthreads();
+    trace_point<MODE>(p, 7);
+    trace_resets<MODE>(p, active, s);
+    // reward (own agent) and state columns
+    if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) {
+        const float r = reward_one(s, k, AGENT0_ID + k);
+        __syncthreads();  // every lane has read the rewards it needs
+        if (lane_used) s.rew[k] = r;
+        __syncthreads();
+    }
+    if (active) {
+        const LaneOrig x = *lo;
+        store_world_agent(s, p, w * N + k, k, &x.agent);
+        if (k == 0) {
+            Orig<N> o;
+            set_world_orig(o, x.world);
+            store_world_shared(s, p, w, &o);
+        }
+    }
+    trace_point<MODE>(p, 8);
+    if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
+
+    // observations: intrinsic block of the lane's agent into the exchange
+    // buffer, then the row in passes through the tile
+    const int32_t ib = inbounder_id(s);
+    const bool share = obs_sharable(s);
+    {
+        ArraySink<INTRINSIC> o;
+        o.idx = 0;
+        emit_intrinsic(s, o, k, attacking_hoop(s, c, k));
+        __syncthreads();  // tile-row (LaneOrig) and exchange-buffer readers are done
+        if (lane_used) {
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) sm.x[lane][q] = fbits(o.v[q]);
+        }
+        __syncthreads();
+    }
+    const bool fast = active && canonical_slots(s, k);
+    if constexpr (MODE == MODE_DIRECT_OBS) {
+        if (active) {
+            float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
+            if (fast) {
+                RowSink o;
+                o.row = grow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                auto intr = [&](int j, int q) { return bitsf(sm.x[slot * N + j][q]); };
+                emit_row_view(s, c, k, intr, share, o, ib);
+            } else {
+                fill_obs_slow(s, c, k, grow, ib);
+            }
+        }
+    } else {
+        if (active && !fast) fill_obs_slow(s, c, k, p.c.obs + (w * N + k) * (int64_t)OW, ib);
+        obs_phases_view<N, MODE>(s, c, k, sm.x, slot, share, fast, tile, w0 * N, lane, ib);
+    }
+    trace_point<MODE>(p, 9);
+}
+
 // One lane per world.
 template <int N, int MODE>
 __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
@@ -465,8 +622,14 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
     __shared__ float4 tile4[tile_floats<N>() / 4];
     start_skew();
-    if constexpr (Lanes<N>::LPW == N) step_agent_lanes<N, MODE>(p, (float *)tile4);
-    else step_world_lanes<N, MODE>(p, (float *)tile4);
+    if constexpr (Lanes<N>::SHARED) {
+        __shared__ SharedLds<N> sm;
+        step_shared_world<N, MODE>(p, (float *)tile4, sm);
+    } else if constexpr (Lanes<N>::LPW == N) {
+        step_agent_lanes<N, MODE>(p, (float *)tile4);
+    } else {
+        step_world_lanes<N, MODE>(p, (float *)tile4);
+    }
 }
 
 template <int N>

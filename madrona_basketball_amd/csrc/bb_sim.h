@@ -185,6 +185,14 @@ BB_HD Q4 uni(Q4 q)
     return r;
 }
 
+// Agent held by slot `slot` of agent k's view: k itself, then the other
+// agents in creation order.
+template <int N>
+BB_HD constexpr int view_source(int slot, int k)
+{
+    return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
+}
+
 // Value of f(j) for j == i, built from selects (i may be a runtime value --
 // e.g. the lane's agent -- while every array index inside f stays constant).
 template <int N, class F>
@@ -1505,6 +1513,47 @@ BB_HD void emit_row_shared(const World<N> &s, const Ctx &c, const SharedObs<N> &
     o.finish();
 }
 
+// Row of observer `a` (a runtime index: the world lives in memory that takes
+// indexed access, e.g. LDS) with every put at a compile-time position: the
+// other agents in creation order are view slots 1..N-1.  intr(j, q) is value
+// q of agent j's intrinsic block measured against j's own attacking hoop;
+// with share (obs_sharable) those are used for every agent, otherwise the
+// other agents' blocks are recomputed against the observer's hoops
+// (bit-identical to emit_row_fast for canonical slot layouts).
+template <int N, class Sink, class IntrOf>
+BB_HD void emit_row_view(const World<N> &s, const Ctx &c, int a, IntrOf intr, bool share, Sink &o, int32_t ib)
+{
+    F3 att, dfn;
+    obs_context(s, c, o, a, &att, &dfn);
+    const F3 p = s.pos(a);
+    o.put3(p);
+    o.put3(f3(0.f, 0.f, 0.f));
+    o.put(0.f);
+#pragma unroll
+    for (int q = 0; q < INTRINSIC; q++) o.put(intr(a, q));
+#pragma unroll
+    for (int t = 1; t < N; t++) {
+        const int j = view_source<N>(t, a);
+        const F3 pj = s.pos(j), to = pj - p;
+        const float l2 = len2(to);
+        const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
+        o.put3(pj);
+        o.put3(l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f));
+        o.put(bbm::sqrtf_(l2));
+        if (share) {
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) o.put(intr(j, q));
+        } else {
+            emit_intrinsic(s, o, j, s.team[j] == s.team[a] ? att : dfn);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
+#pragma unroll
+    for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
+    o.finish();
+}
+
 template <int N>
 BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
 {
@@ -1623,11 +1672,6 @@ BB_HD T pick(const T (&a)[N], int idx)
     return r;
 }
 
-template <int N>
-BB_HD constexpr int view_source(int slot, int k)  // absolute agent held by view slot
-{
-    return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
-}
 
 template <int N>
 BB_HD void agent_view(const World<N> &s, World<N> &v, int k)
@@ -1794,6 +1838,63 @@ BB_HD bool differ(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
 #pragma unroll
     for (int k = 0; k < NW; k++) d |= a[k] != b[k];
     return d;
+}
+
+// The loads of load_world split by owner, for kernels whose N lanes of a
+// world load it together (lane i: agent i's columns; lane 0 also the world's).
+template <int N>
+BB_HD void load_world_shared(World<N> &s, const Params &p, int64_t w)
+{
+    const Columns &c = p.c;
+    uint32_t g[14];
+    load_words<14>(c.game_state, w, g);
+    s.g_inb = (int32_t)g[0]; s.g_live = (int32_t)g[1]; s.g_period = bitsf(g[2]); s.g_poss = bitsf(g[3]);
+    s.g_h0 = (int32_t)g[4]; s.g_s0 = bitsf(g[5]); s.g_h1 = (int32_t)g[6]; s.g_s1 = bitsf(g[7]);
+    s.g_clock = bitsf(g[8]); s.g_shot = bitsf(g[9]); s.g_bask = bitsf(g[10]); s.g_oob = bitsf(g[11]);
+    s.g_inbclk = bitsf(g[12]); s.g_1v1 = (int32_t)g[13];
+    s.reset_now = c.world_clock[w];
+    s.rng_ctr = c.rng_counter[w];
+    const float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
+    s.bx = bp[0]; s.by = bp[1]; s.bz = bp[2];
+    s.bvx = bv[0]; s.bvy = bv[1]; s.bvz = bv[2];
+    const int32_t *ph = c.ball_physics + w * 7;
+    s.fl = ph[0]; s.lta = ph[1]; s.ltt = ph[2]; s.sba = ph[3]; s.sbt = ph[4]; s.spv = ph[5]; s.gin = ph[6];
+    uint32_t gb[2];
+    load_words<2>(c.ball_grabbed, w, gb);
+    s.grab = (int32_t)gb[0]; s.holder = (int32_t)gb[1];
+}
+
+template <int N>
+BB_HD void load_world_agent(World<N> &s, const Params &p, int64_t w, int i)
+{
+    const Columns &c = p.c;
+    const int64_t r = w * N + i;
+    uint32_t a[6], pos[3], ps[3], q[4], v[3], ib[2], at[10];
+    load_words<6>(c.action, r, a);
+    load_words<3>(c.agent_pos, r, pos);
+    load_words<3>(c.possession, r, ps);
+    load_words<4>(c.orientation, r, q);
+    load_words<3>(c.agent_vel, r, v);
+    load_words<2>(c.inbounding, r, ib);
+    load_words<10>(c.attributes, r, at);
+    s.rst[i] = c.reset[r];
+#pragma unroll
+    for (int k = 0; k < 6; k++) s.act[i][k] = (int32_t)a[k];
+    s.px[i] = bitsf(pos[0]); s.py[i] = bitsf(pos[1]); s.pz[i] = bitsf(pos[2]);
+    s.has[i] = (int32_t)ps[0]; s.bid[i] = (int32_t)ps[1]; s.pw[i] = (int32_t)ps[2];
+    s.qw[i] = bitsf(q[0]); s.qx[i] = bitsf(q[1]); s.qy[i] = bitsf(q[2]); s.qz[i] = bitsf(q[3]);
+    s.vx[i] = bitsf(v[0]); s.vy[i] = bitsf(v[1]); s.vz[i] = bitsf(v[2]);
+    s.cd[i] = c.cooldown[r];
+    s.step[i] = c.cur_step[r];
+    s.inb[i] = (int32_t)ib[0]; s.allow[i] = (int32_t)ib[1];
+#pragma unroll
+    for (int k = 0; k < 10; k++) s.attr[i][k] = bitsf(at[k]);
+    const uint32_t *t = c.team + r * 5;
+    s.team[i] = (int32_t)t[0];
+    s.dhoop[i] = (int32_t)t[4];
+    s.rew[i] = 0.f; s.done[i] = 0.f;  // rewritten by tick before any read
+#pragma unroll
+    for (int k = 0; k < 4; k++) s.msk[i][k] = 0;  // rewritten by actionMaskSystem
 }
 
 // World-level columns (GameState, WorldClock, RNG counter, ball).  With `o`,

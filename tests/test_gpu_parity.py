@@ -81,12 +81,36 @@ def test_gpu_equals_host_executor_bitwise():
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), n
 
 
-@pytest.mark.parametrize("n_agents", [4, 10])
+@pytest.mark.parametrize("n_agents", [4, 6, 8, 10])
 def test_gpu_more_agents(n_agents):
-    W = 1024
+    """N >= 4 runs the shared-LDS-world kernel (one lane per agent); 1000
+    worlds leave a partly filled last wave for every N."""
+    W = 1000
     sim = make_sim(ExecMode.CUDA, W, num_agents=n_agents, per_world_rng=True)
     o = Oracle(W, num_agents=n_agents, flags=oracle_flags(per_world_rng=True))
     run_lockstep(sim, o, 400, check_every=100)
+
+
+@pytest.mark.parametrize("n_agents", [4, 10])
+@pytest.mark.parametrize("flags", [dict(tag_mask=False), dict(one_on_one=False, tag_mask=False)])
+def test_gpu_more_agents_variants(n_agents, flags):
+    """Grab / pass / steal and the full-game rules with N agents on the GPU."""
+    W = 600
+    sim = make_sim(ExecMode.CUDA, W, num_agents=n_agents, per_world_rng=True, **flags)
+    o = Oracle(W, num_agents=n_agents, flags=oracle_flags(per_world_rng=True, **flags))
+    run_lockstep(sim, o, 300, check_every=50)
+
+
+@pytest.mark.parametrize("n_agents", [4, 10])
+def test_gpu_more_agents_equal_host_executor(n_agents):
+    W = 700
+    g = make_sim(ExecMode.CUDA, W, num_agents=n_agents, per_world_rng=True)
+    h = make_sim(ExecMode.CPU, W, num_agents=n_agents, per_world_rng=True)
+    g.step_n(250, random_actions=True)
+    h.step_n(250, random_actions=True)
+    torch.cuda.synchronize()
+    for name in g._views:
+        assert torch.equal(g._views[name].cpu(), h._views[name]), name
 
 
 @pytest.mark.parametrize("flags", [dict(tag_mask=False), dict(one_on_one=False), dict(tag_mask=False, one_on_one=False)])
