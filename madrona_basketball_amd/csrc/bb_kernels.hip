@@ -46,13 +46,11 @@ struct ObsTile {
 #ifndef BB_AGENT_LANES
 #define BB_AGENT_LANES 1
 #endif
-#ifndef BB_LDS_MIN_N
-#define BB_LDS_MIN_N 4  // from this agent count on, the world state lives in LDS
-#endif
 template <int N>
 struct Lanes {
-    // SHARED: one lane per agent, the world's state in LDS shared by its N lanes
-    static constexpr bool SHARED = N >= BB_LDS_MIN_N;
+    // SHARED: one lane per agent, the world's state in LDS shared by its N
+    // lanes (pick_by indexes directly from the same N on, bb_sim.h)
+    static constexpr bool SHARED = N >= LDS_WORLD_MIN_N;
     static constexpr int LPW = SHARED ? N : ((BB_AGENT_LANES && (N == 2 || N == 4)) ? N : 1);
     static constexpr int WPB = WAVE / LPW;  // worlds per 64-lane workgroup
 };

@@ -193,15 +193,25 @@ BB_HD constexpr int view_source(int slot, int k)
     return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
 }
 
-// Value of f(j) for j == i, built from selects (i may be a runtime value --
-// e.g. the lane's agent -- while every array index inside f stays constant).
+// From this agent count on the GPU kernel keeps the world in LDS
+// (bb_kernels.hip, Lanes::SHARED), where an indexed access is one LDS load.
+constexpr int LDS_WORLD_MIN_N = 4;
+
+// Value of f(j) for j == i.  For register-resident worlds (N < 4) it is built
+// from selects: i may be a runtime value -- e.g. the lane's agent -- while
+// every array index inside f stays constant, so nothing goes to scratch.  For
+// worlds in LDS (and on the host) f(i) indexes directly.
 template <int N, class F>
 BB_HD auto pick_by(int i, F f) -> decltype(f(0))
 {
-    auto r = f(0);
+    if constexpr (N >= LDS_WORLD_MIN_N) {
+        return f(i);
+    } else {
+        auto r = f(0);
 #pragma unroll
-    for (int j = 1; j < N; j++) r = sel(i == j, f(j), r);
-    return r;
+        for (int j = 1; j < N; j++) r = sel(i == j, f(j), r);
+        return r;
+    }
 }
 
 // How per-agent work is spread over lanes.  EachAgent: the calling lane
