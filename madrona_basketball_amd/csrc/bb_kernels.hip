@@ -437,6 +437,14 @@ __device__ __forceinline__ void obs_phases_view(const World<N> &s, const Ctx &c,
     }
 }
 
+#ifndef BB_SHARED_TILE
+#define BB_SHARED_TILE 0
+#endif
+template <int N>
+struct SharedTiled {
+    static constexpr bool value = BB_SHARED_TILE != 0;
+};
+
 template <int N, int MODE>
 __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm)
 {
@@ -461,18 +469,16 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         if (k == 0) load_world_shared(s, p, w);
     }
     __syncthreads();
-    // event-only words as loaded, parked in the lane's tile row
-    LaneOrig *lo = (LaneOrig *)(tile + lane * PhasedTile<N>::RS);
+    // event-only words as loaded (store only on change, see Orig)
+    LaneOrig lo;
     if (active) {
         Orig<N> o;
         game_words(s, o.game);
         phys_words(s, o.phys);
         o.grab[0] = (uint32_t)s.grab; o.grab[1] = (uint32_t)s.holder;
         o.clock = (uint32_t)s.reset_now; o.rng = s.rng_ctr;
-        LaneOrig x;
-        x.world = world_orig(o);
-        x.agent = orig_agent(s, k);
-        *lo = x;
+        lo.world = world_orig(o);
+        lo.agent = orig_agent(s, k);
     }
     if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, 0u);
     else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
@@ -487,11 +493,10 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();
     }
     if (active) {
-        const LaneOrig x = *lo;
-        store_world_agent(s, p, w * N + k, k, &x.agent);
+        store_world_agent(s, p, w * N + k, k, &lo.agent);
         if (k == 0) {
             Orig<N> o;
-            set_world_orig(o, x.world);
+            set_world_orig(o, lo.world);
             store_world_shared(s, p, w, &o);
         }
     }
@@ -506,7 +511,7 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         ArraySink<INTRINSIC> o;
         o.idx = 0;
         emit_intrinsic(s, o, k, attacking_hoop(s, c, k));
-        __syncthreads();  // tile-row (LaneOrig) and exchange-buffer readers are done
+        __syncthreads();  // exchange-buffer readers are done
         if (lane_used) {
 #pragma unroll
             for (int q = 0; q < INTRINSIC; q++) sm.x[lane][q] = fbits(o.v[q]);
@@ -514,7 +519,9 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();
     }
     const bool fast = active && canonical_slots(s, k);
-    if constexpr (MODE == MODE_DIRECT_OBS) {
+    // rows straight from the lanes (no tile: the LDS goes to occupancy) unless
+    // BB_SHARED_TILE stages them
+    if constexpr (MODE == MODE_DIRECT_OBS || !SharedTiled<N>::value) {
         if (active) {
             float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
             if (fast) {
@@ -595,6 +602,7 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
 template <int N>
 constexpr int tile_floats()
 {
+    if constexpr (Lanes<N>::SHARED) return BB_SHARED_TILE ? PhasedTile<N>::FLOATS : 4;
     return Lanes<N>::LPW == N ? PhasedTile<N>::FLOATS : ObsTile<N>::FLOATS;
 }
 

@@ -49,6 +49,8 @@ for s in $STEPS; do
     bench10) run bench10 600 python bench.py --agents 10 --steps 100 --warmup 20 --no-cpu-baseline ;;
     ablate) run ablate 600 python tools/ablate.py --worlds 65536 ;;
     ablate262k) run ablate262k 600 python tools/ablate.py --worlds 262144 --iters 50 ;;
+    ablate4) run ablate4 600 python tools/ablate.py --worlds 65536 --agents 4 --iters 30 --rounds 3 ;;
+    ablate10) run ablate10 600 python tools/ablate.py --worlds 65536 --agents 10 --iters 10 --rounds 3 ;;
     systems) run systems 600 python tools/ablate_systems.py --worlds 65536 ;;
     pmcab) run pmcab 900 bash tools/pmc_ablate.sh "$TAG/pmc" 65536 ;;
     prof)
@@ -69,6 +71,9 @@ for s in $STEPS; do
               run "pmc_${v}_$c" 300 rocprofv3 --pmc $c -d "$OUT/pmc_${v}_$c" -o run --output-format csv -- \
                 python3 "$ROOT/tools/ablate.py" --worlds 65536 --iters 20 --rounds 1 --only 0 ) || exit $?
         done ;;
+    abn:*) v=${s#abn:}; n=${v#*:}; v=${v%%:*}
+        MADRONA_BB_LIB=$ROOT/madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so \
+            run "ablate_${v}_n$n" 600 python tools/ablate.py --worlds 65536 --agents $n --iters 10 --rounds 3 --only 0 1 2 4 ;;
     ab:*) v=${s#ab:}
         MADRONA_BB_LIB=$ROOT/madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so \
             run "ablate_$v" 600 python tools/ablate.py --worlds 65536 ;;
