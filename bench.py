@@ -88,6 +88,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-procs", type=int, default=min(16, os.cpu_count() or 1),
                     help="host processes for the CPU baseline (the GPU box's share is 16 cores)")
+    ap.add_argument("--rollout", type=int, default=0,
+                    help="K > 0: bb_rollout of K steps per call (observations / rewards / dones recorded "
+                         "into [K, W, N, ...] buffers; one k_rollout launch at 2 agents); 0: one step per call")
+    ap.add_argument("--no-record", action="store_true",
+                    help="diagnostics: rollouts without recorded outputs (each step rewrites the sim's own tensors)")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
@@ -115,6 +120,7 @@ def main():
 
     import madrona_basketball_amd as mba
     from madrona_basketball_amd import _lib
+    fused = bool(_lib.load().bb_rollout_fused(args.agents)) if on_gpu else False
 
     W = args.worlds
     sim = mba.SimpleGridworldSimulator(
@@ -146,9 +152,29 @@ def main():
     staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup)
     barrier()
 
+    K = args.rollout
+    if K:
+        if args.steps % K:
+            raise SystemExit("--steps must be a multiple of --rollout")
+        bufs = sim.rollout_buffers(K)  # reused by every chunk, like PPO's storage between updates
+
+    def run(actions, time_kernels=False):
+        """All staged steps: one step per launch, or chunks of K via bb_rollout."""
+        if not K:
+            return sim.step_n_staged(actions, time_kernels=time_kernels)
+        ms = 0.0
+        for i in range(0, args.steps, K):
+            if args.no_record:
+                r = sim.rollout(actions[i:i + K], time_kernels=time_kernels)
+            else:
+                r = sim.rollout(actions[i:i + K], bufs["obs"], bufs["reward"], bufs["done"],
+                                time_kernels=time_kernels)
+            ms += r or 0.0
+        return ms
+
     # timed region: exactly K steps, step k reading staged[k] (scripts/run.py:10-15)
     t0 = time.perf_counter()
-    sim.step_n_staged(staged)
+    run(staged)
     sync()
     elapsed = time.perf_counter() - t0
     barrier()
@@ -156,21 +182,29 @@ def main():
 
     # kernel timing: the step kernel's own start/end (hipExtLaunchKernel
     # events on the launch stream) over the same workload, re-staged
+    launches = args.steps // K if (K and fused) else args.steps
     if on_gpu:
         staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup + args.steps)
         barrier()
-        kernel_ms = sim.step_n_staged(staged, time_kernels=True)
+        kernel_ms = run(staged, time_kernels=True)
         barrier()
-        avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / args.steps)
+        avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / launches)
     else:
-        avg_kernel_s = elapsed / args.steps
+        avg_kernel_s = elapsed / launches
     del staged
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
-    bytes_per_launch = _lib.load().bb_algorithmic_bytes_per_world(args.agents) * W
+    L = _lib.load()
+    if K and fused:
+        # per launch: the state once in and out, and per step only the action
+        # rows in and the recorded rows (obs, reward, done) out
+        bytes_per_launch = W * (K * L.bb_rollout_bytes_per_world_step(args.agents)
+                                + L.bb_rollout_state_bytes_per_world(args.agents))
+    else:
+        bytes_per_launch = L.bb_algorithmic_bytes_per_world(args.agents) * W
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
-    workload_key = f"W{W}_N{args.agents}"
+    workload_key = f"W{W}_N{args.agents}" + (f"_R{K}" if K else "")
     traffic = load_traffic(workload_key)
 
     out = {
@@ -189,7 +223,9 @@ def main():
         "config": {
             "workload": f"{W} worlds per GPU x {args.agents} agents (reference 1v1 game, "
                         f"NUM_AGENTS={args.agents}), threefry random actions per step (buckets "
-                        f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG",
+                        f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
+                        + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
+                           f"of every step recorded into [{K}, W, N, ...] buffers" if K else "; one step per call"),
             "worlds_per_gpu": W,
             "total_worlds": total_worlds,
             "agents_per_world": args.agents,
@@ -202,7 +238,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "bb::k_step<%d>" % args.agents,
+            "kernel": ("bb::k_rollout<%d>" if (K and fused) else "bb::k_step<%d>") % args.agents,
             "kernel_avg_us": avg_kernel_s * 1e6,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },

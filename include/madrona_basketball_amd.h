@@ -15,6 +15,9 @@
  *   bb_step_n_staged    <- n x (actions[:] = a_k; Manager::step), the
  *                          scripts/run.py:10-15 loop with a_k staged in HBM
  *   bb_fill_random_actions <- (new) stages a_k for bb_step_n_staged
+ *   bb_rollout          <- n x (actions[:] = a_k; Manager::step; copy of
+ *                          observations/rewards/dones), the rollout loop of
+ *                          scripts/ppo.py:139-176 with a_k staged in HBM
  *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
  *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
  *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
@@ -161,6 +164,26 @@ int bb_step_n_staged(bb_sim *sim, int32_t n, int32_t *actions, void *stream, flo
 int bb_fill_random_actions(bb_sim *sim, int32_t *actions, int32_t n, uint32_t action_seed, uint32_t step0,
                            void *stream);
 
+/* bb_rollout flags */
+#define BB_ROLLOUT_PER_STEP 0x1u /* one step kernel launch per step, state through HBM
+                                    (default on gfx950 at 2 agents: one launch for all
+                                    steps, the worlds held in registers) */
+
+/* n-step rollout.  Equivalent to, for k = 0..n-1:
+ *     action tensor := actions[k]; bb_step();
+ *     obs_out[k] := observations; reward_out[k] := reward; done_out[k] := done
+ * with the defence AI's overrides written back into actions[k] (as
+ * bb_step_n_staged).  Layouts: actions int32 [n][W][N][6], obs_out float
+ * [n][W][N][obs_width], reward_out/done_out float [n][W][N], on the
+ * simulator's device (host memory in CPU mode).  Observation columns from
+ * roundup4(61 + 38(N-1) + 2N) on are never written: zero obs_out once.  A
+ * NULL output is not recorded (that tensor of the simulator is rewritten
+ * every step instead).  Afterwards every simulator column holds the state
+ * after step n-1 (observations, reward, done and action included).
+ * kernel_ms as in bb_step_n (summed over the launches). */
+int bb_rollout(bb_sim *sim, int32_t n, int32_t *actions, float *obs_out, float *reward_out, float *done_out,
+               uint32_t flags, void *stream, float *kernel_ms);
+
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,
                   int32_t shoot, void *stream);
@@ -179,6 +202,15 @@ int32_t bb_exec_mode(const bb_sim *sim);
 
 /* Algorithmic HBM bytes moved by one step of one world (roofline). */
 int64_t bb_algorithmic_bytes_per_world(int32_t num_agents);
+
+/* 1 if bb_rollout runs as one fused launch (gfx950) for num_agents. */
+int32_t bb_rollout_fused(int32_t num_agents);
+
+/* Algorithmic HBM bytes of a fused rollout (roofline): per world
+ * and step (action row in, observation row + reward + done out), and per
+ * world and launch (the remaining state columns, in once and out once). */
+int64_t bb_rollout_bytes_per_world_step(int32_t num_agents);
+int64_t bb_rollout_state_bytes_per_world(int32_t num_agents);
 
 /* Message for the last error on this thread ("" if none). */
 const char *bb_last_error(void);

@@ -21,6 +21,7 @@ DTYPE_FLOAT32 = 1
 FLAG_PER_WORLD_RNG = 0x1
 FLAG_NO_TAG_MASK = 0x2
 FLAG_FULL_GAME = 0x4
+ROLLOUT_PER_STEP = 0x1
 NUM_REFERENCE_EXPORTS = 19
 INTERNAL_FIRST = 32
 INTERNAL_LAST = 38
@@ -40,8 +41,10 @@ EXPORT_IDS = {
 ABI_SYMBOLS = [
     "bb_default_config", "bb_obs_width", "bb_buffer_bytes", "bb_create",
     "bb_create_with_buffers", "bb_destroy", "bb_step", "bb_step_n",
-    "bb_write_random_actions", "bb_step_n_staged", "bb_fill_random_actions", "bb_set_action", "bb_trigger_reset", "bb_export",
+    "bb_write_random_actions", "bb_step_n_staged", "bb_fill_random_actions", "bb_rollout",
+    "bb_set_action", "bb_trigger_reset", "bb_export",
     "bb_num_worlds", "bb_num_agents", "bb_exec_mode", "bb_algorithmic_bytes_per_world",
+    "bb_rollout_fused", "bb_rollout_bytes_per_world_step", "bb_rollout_state_bytes_per_world",
     "bb_last_error",
 ]
 
@@ -91,6 +94,7 @@ def load():
         "bb_write_random_actions": (ctypes.c_int, [vp, u32, u32, vp]),
         "bb_step_n_staged": (ctypes.c_int, [vp, i32, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "bb_fill_random_actions": (ctypes.c_int, [vp, vp, i32, u32, u32, vp]),
+        "bb_rollout": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, u32, vp, ctypes.POINTER(ctypes.c_float)]),
         "bb_set_action": (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "bb_trigger_reset": (ctypes.c_int, [vp, i32, vp]),
         "bb_export": (ctypes.c_int, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(i32),
@@ -99,6 +103,9 @@ def load():
         "bb_num_agents": (i32, [vp]),
         "bb_exec_mode": (i32, [vp]),
         "bb_algorithmic_bytes_per_world": (i64, [i32]),
+        "bb_rollout_fused": (i32, [i32]),
+        "bb_rollout_bytes_per_world_step": (i64, [i32]),
+        "bb_rollout_state_bytes_per_world": (i64, [i32]),
         "bb_last_error": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():

@@ -14,9 +14,13 @@ CSRC = os.path.join(HERE, "csrc")
 LIB_NAME = "libmadrona_basketball_amd.so"
 LIB_PATH = os.path.join(HERE, LIB_NAME)
 AGENT_COUNTS = [2, 4, 6, 8, 10]
+# MachineLICM hoists the f64 polynomial constants of bb_math.h out of
+# k_rollout's step loop and then spills them (628 B/lane of scratch); without
+# it they are rematerialised in place.  k_step is unaffected (same VGPRs).
+KERNEL_FLAGS = ["-mllvm", "-disable-machine-licm"]
 # (source, extra flags, object name): the step kernel once per agent count,
 # compiled in parallel
-UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}"], f"bb_kernels_n{n}.o") for n in AGENT_COUNTS]
+UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}", *KERNEL_FLAGS], f"bb_kernels_n{n}.o") for n in AGENT_COUNTS]
          + [("bb_common.hip", [], "bb_common.o"), ("bb_host.hip", [], "bb_host.o")])
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = ["bb_math.h", "bb_rng.h", "bb_sim.h", "bb_launch.h"]

@@ -104,6 +104,25 @@ int step_grid_n(int n, int64_t num_worlds)
 #undef CALL
 }
 
+hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
+{
+#define CALL(k) launch_rollout_t<k>(p, r, s, ev0, ev1)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
+bool fused_rollout_n(int n)
+{
+    switch (n) {
+    case 2: return fused_rollout<2>();
+    case 4: return fused_rollout<4>();
+    case 6: return fused_rollout<6>();
+    case 8: return fused_rollout<8>();
+    case 10: return fused_rollout<10>();
+    default: return false;
+    }
+}
+
 hipError_t launch_init(int n, const Params &p, hipStream_t s)
 {
 #define CALL(k) launch_init_t<k>(p, s)

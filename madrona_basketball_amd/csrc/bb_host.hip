@@ -562,6 +562,102 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     return BB_OK;
 }
 
+int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *reward_out, float *done_out,
+               uint32_t flags, void *stream, float *kernel_ms)
+{
+    if (!s || n < 0 || (!actions && n > 0)) return fail(BB_ERR_INVALID_ARG, "bb_rollout");
+    if (flags & ~BB_ROLLOUT_PER_STEP) return fail(BB_ERR_INVALID_ARG, "bb_rollout: unknown flag bits");
+    if (kernel_ms) *kernel_ms = 0.f;
+    if (n == 0) return BB_OK;
+    const int64_t rows = s->cfg.num_worlds * s->n;  // [W][N]
+    const int64_t ow = bb::obs_width(s->n);
+    const int64_t used_bytes = (int64_t)((bb::obs_used(s->n) + 3) / 4) * 16;  // written part of a row
+    bb::RolloutArgs r;
+    r.actions = actions;
+    r.obs = obs_out ? obs_out : s->p.c.obs;
+    r.reward = reward_out ? reward_out : s->p.c.reward;
+    r.done = done_out ? done_out : s->p.c.done;
+    r.obs_step = obs_out ? rows * ow : 0;
+    r.rd_step = (reward_out || done_out) ? rows : 0;
+    if ((reward_out == nullptr) != (done_out == nullptr))
+        return fail(BB_ERR_INVALID_ARG, "bb_rollout: reward_out and done_out are recorded together");
+    r.steps = n;
+    const float *last_obs = r.obs + (int64_t)(n - 1) * r.obs_step;
+    const float *last_rew = r.reward + (int64_t)(n - 1) * r.rd_step;
+    const float *last_done = r.done + (int64_t)(n - 1) * r.rd_step;
+    const int32_t *last_act = actions + (int64_t)(n - 1) * rows * 6;
+    auto step_params = [&](int32_t k) {
+        bb::Params pp = s->p;
+        pp.c.action = actions + (int64_t)k * rows * 6;
+        pp.c.obs = r.obs + (int64_t)k * r.obs_step;
+        pp.c.reward = r.reward + (int64_t)k * r.rd_step;
+        pp.c.done = r.done + (int64_t)k * r.rd_step;
+        return pp;
+    };
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) {
+        for (int32_t k = 0; k < n; k++) {
+            int rc = bb::host_step(s->n, step_params(k), host_threads_for(s->cfg.num_worlds));
+            if (rc != BB_OK) return rc;
+        }
+        std::memcpy(s->p.c.action, last_act, (size_t)rows * 24);
+        if (obs_out)
+            for (int64_t q = 0; q < rows; q++) std::memcpy(s->p.c.obs + q * ow, last_obs + q * ow, (size_t)used_bytes);
+        if (reward_out) {
+            std::memcpy(s->p.c.reward, last_rew, (size_t)rows * 4);
+            std::memcpy(s->p.c.done, last_done, (size_t)rows * 4);
+        }
+        return BB_OK;
+    }
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    const bool fused = !(flags & BB_ROLLOUT_PER_STEP) && bb::fused_rollout_n(s->n);
+    const int32_t launches = fused ? 1 : n;
+    std::vector<hipEvent_t> ev;
+    if (kernel_ms) {
+        ev.resize((size_t)2 * launches);
+        for (auto &e : ev) {
+            hipError_t he = hipEventCreate(&e);
+            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
+        }
+    }
+    hipEvent_t *evp = ev.empty() ? nullptr : ev.data();
+    if (fused) {
+        hipError_t e = bb::launch_rollout(s->n, s->p, r, st, evp ? evp[0] : nullptr, evp ? evp[1] : nullptr);
+        if (e != hipSuccess) return hip_fail(e, "launch rollout kernel");
+    } else {
+        for (int32_t k = 0; k < n; k++) {
+            hipError_t e = bb::launch_step(s->n, step_params(k), st, bb::MODE_FULL, evp ? evp[2 * k] : nullptr,
+                                           evp ? evp[2 * k + 1] : nullptr);
+            if (e != hipSuccess) return hip_fail(e, "launch step kernel");
+        }
+        hipError_t e = hipMemcpyAsync(s->p.c.action, last_act, (size_t)rows * 24, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return hip_fail(e, "copy last actions");
+        if (reward_out) {
+            e = hipMemcpyAsync(s->p.c.reward, last_rew, (size_t)rows * 4, hipMemcpyDeviceToDevice, st);
+            if (e == hipSuccess) e = hipMemcpyAsync(s->p.c.done, last_done, (size_t)rows * 4, hipMemcpyDeviceToDevice, st);
+            if (e != hipSuccess) return hip_fail(e, "copy last reward/done");
+        }
+    }
+    if (obs_out) {  // the written part of every row (the zero tail stays)
+        hipError_t e = hipMemcpy2DAsync(s->p.c.obs, (size_t)ow * 4, last_obs, (size_t)ow * 4, (size_t)used_bytes,
+                                        (size_t)rows, hipMemcpyDeviceToDevice, st);
+        if (e != hipSuccess) return hip_fail(e, "copy last observations");
+    }
+    if (!ev.empty()) {
+        hipError_t e = hipEventSynchronize(ev.back());
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        double total = 0.0;
+        for (int32_t k = 0; k < launches; k++) {
+            float ms = 0.f;
+            (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
+            total += ms;
+        }
+        for (auto &x : ev) (void)hipEventDestroy(x);
+        *kernel_ms = (float)total;
+    }
+    return BB_OK;
+}
+
 int bb_set_action(bb_sim *s, int32_t world_idx, int32_t agent_idx, int32_t move_speed, int32_t move_angle,
                   int32_t rotate, int32_t grab, int32_t pass, int32_t shoot, void *stream)
 {
@@ -691,6 +787,22 @@ int64_t bb_algorithmic_bytes_per_world(int32_t n)
 {
     // B(N) = N (268 + 4 obs_used(N)) + 152
     return (int64_t)n * (268 + 4 * (int64_t)bb::obs_used(n)) + 152;
+}
+
+int32_t bb_rollout_fused(int32_t n) { return bb::fused_rollout_n(n) ? 1 : 0; }
+
+int64_t bb_rollout_bytes_per_world_step(int32_t n)
+{
+    // per step and agent: action row in (24 B), observation row (4 obs_used),
+    // reward and done (8 B) out
+    return (int64_t)n * (32 + 4 * (int64_t)bb::obs_used(n));
+}
+
+int64_t bb_rollout_state_bytes_per_world(int32_t n)
+{
+    // once per launch: the B(N) state columns except the per-step action read
+    // and observation write (loaded at the start, stored after the last step)
+    return bb_algorithmic_bytes_per_world(n) - (int64_t)n * (24 + 4 * (int64_t)bb::obs_used(n));
 }
 
 const char *bb_last_error(void) { return g_err.c_str(); }

@@ -29,6 +29,29 @@ namespace bb {
 
 constexpr int WAVE = 64;
 
+// The erf Taylor table (bb_math.h) copied to LDS by the workgroup's one
+// wave (k_rollout): shotPercentage's per-lane coefficient reads become LDS
+// reads instead of memory loads, which, issued after a step's stores, would
+// wait for all of them (the vector-memory counter retires in order).  k_step
+// reads the table from memory: there no store precedes the read, and the
+// copy's wait would serialise the state loads.
+constexpr int ERF_WORDS = bbm::ERF_TK * (bbm::ERF_TD + 1);
+#ifndef BB_ERF_LDS
+#define BB_ERF_LDS 1
+#endif
+__device__ __forceinline__ const double *erf_table_lds()
+{
+    if constexpr (!BB_ERF_LDS) return &bbm::ERF_TAYLOR[0][0];
+    __shared__ double tab[ERF_WORDS];
+    const double *g = &bbm::ERF_TAYLOR[0][0];
+#pragma unroll
+    for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
+        const int i = j * WAVE + (int)threadIdx.x;
+        if (i < ERF_WORDS) tab[i] = g[i];
+    }
+    return tab;
+}
+
 template <int N>
 struct ObsTile {
     static constexpr int QW = (obs_used(N) + 3) / 4;  // float4 pieces of a used row
@@ -60,16 +83,30 @@ struct Lanes {
 #ifndef BB_OBS_WRITE_ALIGN
 #define BB_OBS_WRITE_ALIGN 16  // bytes: row writes end on this boundary (zero pieces added)
 #endif
-template <int N>
+#ifndef BB_OBS_PHASE_PIECES
+#define BB_OBS_PHASE_PIECES 15  // at most this many 16-byte pieces of a row per pass
+#endif
+// ALIGN: row writes end on this byte boundary (zero pieces added);
+// MAXP: at most this many 16-byte pieces of a row per pass.
+template <int N, int ALIGN = BB_OBS_WRITE_ALIGN, int MAXP = BB_OBS_PHASE_PIECES>
 struct PhasedTile {
     static constexpr int QU = (obs_used(N) + 3) / 4;  // pieces holding row values
-    static constexpr int QA = (QU * 16 + BB_OBS_WRITE_ALIGN - 1) / BB_OBS_WRITE_ALIGN * BB_OBS_WRITE_ALIGN / 16;
+    static constexpr int QA = (QU * 16 + ALIGN - 1) / ALIGN * ALIGN / 16;
     static constexpr int QW = QA < obs_width(N) / 4 ? QA : obs_width(N) / 4;  // pieces written
-    static constexpr int PH = (QW + 14) / 15;
+    static constexpr int PH = (QW + MAXP - 1) / MAXP;
     static constexpr int QP = (QW + PH - 1) / PH;
     static constexpr int RS = QP * 4 + (QP % 2 == 0 ? 4 : 0);  // == 4 mod 8 dwords
     static constexpr int FLOATS = WAVE * RS;
 };
+
+// k_rollout's rows go to a fresh [K][W][N][OBSW] buffer far larger than the
+// Infinity Cache: every 128-byte line is written whole by one pass (passes of
+// 16 pieces = 2 lines per row, the zero tail included), since lines left
+// partial by a pass reach memory as partial writes (measured: 25.7 -> 18.1 us
+// per step at 65 536 worlds).  k_step's 64 MiB rows stay cache-resident,
+// where the 416 written bytes of 2 x 13 pieces are cheaper.
+template <int N>
+using RolloutTile = PhasedTile<N, 128, 16>;
 
 // RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
 // Indices are compile-time after unrolling, so the window test folds away and
@@ -248,11 +285,10 @@ struct Intrinsic {
 };
 
 // Pass PHASE of the lane's row into its tile row (shared path or fast path).
-template <int N, int PHASE>
+template <int N, class T, int PHASE>
 __device__ __forceinline__ void emit_phase(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
                                            float *trow, int32_t ib)
 {
-    using T = PhasedTile<N>;
     constexpr int LO = PHASE * T::QP * 4, HI = LO + T::QP * 4;
     WindowSink<LO, HI> o;
     o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
@@ -260,19 +296,18 @@ __device__ __forceinline__ void emit_phase(const World<N> &v, const Ctx &c, cons
     else emit_row_fast(v, c, 0, o, ib);
 }
 
-template <int N, int MODE, int PHASE = 0>
+template <int N, int MODE, class T, int PHASE = 0>
 __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
-                                           bool fast, float *tile, int64_t row0, int lane, int32_t ib)
+                                           bool fast, float *tile, float *obs, int64_t row0, int lane, int32_t ib)
 {
-    using T = PhasedTile<N>;
-    if (fast) emit_phase<N, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
+    if (fast) emit_phase<N, T, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     __syncthreads();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
     constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
-    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ>(tile, c.p->c.obs, row0, __ballot(fast), lane);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ>(tile, obs, row0, __ballot(fast), lane);
     if constexpr (PHASE + 1 < T::PH) {
         __syncthreads();
-        obs_phases<N, MODE, PHASE + 1>(v, c, sh, share, fast, tile, row0, lane, ib);
+        obs_phases<N, MODE, T, PHASE + 1>(v, c, sh, share, fast, tile, obs, row0, lane, ib);
     }
 }
 
@@ -281,6 +316,59 @@ struct LaneOrig {
     OrigAgent agent;
 };
 static_assert(sizeof(LaneOrig) <= 4 * 52, "fits a row of the observation tile");
+
+// Observation rows of the agent-lane kernel into obs (a [W][N][OBSW] base):
+// the lane's intrinsic block, exchanged with the world's lanes by DPP, then
+// the row through the LDS tile (fast rows) or directly (slow rows).
+// ib / share: inbounder_id and obs_sharable of the world in creation order.
+template <int N, int MODE, class T = PhasedTile<N>>
+__device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
+                                               int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
+{
+    constexpr int OW = obs_width(N);
+    SharedObs<N> sh;
+    if (active) {
+        Intrinsic mine, slot[N];
+        {
+            ArraySink<INTRINSIC> o;
+            o.idx = 0;
+            emit_intrinsic(v, o, 0, attacking_hoop(v, c, 0));
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) mine.v[q] = o.v[q];
+        }
+        lane_gather_view<N>(mine, slot);
+#pragma unroll
+        for (int t = 0; t < N; t++)
+#pragma unroll
+            for (int q = 0; q < INTRINSIC; q++) sh.intr[t].v[q] = slot[t].v[q];
+#pragma unroll
+        for (int t = 1; t < N; t++) {
+            const F3 to = v.pos(t) - v.pos(0);
+            const float l2 = len2(to);
+            const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
+            sh.rdir[0][t] = l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f);
+            sh.rlen[0][t] = bbm::sqrtf_(l2);
+        }
+    }
+    float *grow = obs + (w * N + k) * (int64_t)OW;
+    const bool fast = active && canonical_slots(v, 0);
+    if constexpr (MODE == MODE_DIRECT_OBS) {
+        if (active) {
+            if (share) {
+                RowSink o;
+                o.row = grow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                emit_row_shared(v, c, sh, 0, o, ib);
+            } else if (fast) {
+                fill_obs_fast(v, c, 0, grow, ib);
+            } else {
+                fill_obs_slow(v, c, 0, grow, ib);
+            }
+        }
+    } else {
+        if (active && !fast) fill_obs_slow(v, c, 0, grow, ib);
+        obs_phases<N, MODE, T>(v, c, sh, share, fast, tile, obs, w0 * N, lane, ib);
+    }
+}
 
 // One lane per agent: lane = (w - w0) * N + k.
 template <int N, int MODE>
@@ -333,52 +421,134 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
 
-    // intrinsic block of the lane's agent, exchanged with the world's lanes
     const int32_t ib = active ? inbounder_id(s) : -1;
     const bool share = active && obs_sharable(s);
-    SharedObs<N> sh;
+    agent_lane_obs<N, MODE>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+    trace_point<MODE>(p, 9);
+}
+
+// ------------------------------------------------------------------ rollout
+// K steps in one launch (agent lanes, N = 2): the world stays in registers
+// from the first load to the last store, so a step moves only its action
+// rows in and its observation rows, rewards and done flags out -- exactly
+// what K launches of k_step would leave in those buffers (bb_rollout).
+// Step t+1's action rows are loaded before step t's stores are issued, so
+// the stores of one step drain while the next one's systems run.
+template <int N>
+struct FusedRollout {
+    static constexpr bool value = Lanes<N>::LPW == N && !Lanes<N>::SHARED;
+};
+
+template <int N>
+__device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile)
+{
+    using T = RolloutTile<N>;
+    static_assert(T::RS >= 6, "a tile row parks the lane's staged action row");
+    const int lane = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
+    const int64_t rows = p.num_worlds * N;  // [W][N] rows per step
+
+    // Between steps only the lane's view of the world is live (agent k in
+    // slot 0); each step rebuilds the creation-order world from it, so the
+    // systems' and the observation pass's register sets never overlap.
+    World<N> v;
+    uint32_t a_next[6 * N];
     if (active) {
-        Intrinsic mine, slot[N];
-        {
-            ArraySink<INTRINSIC> o;
-            o.idx = 0;
-            emit_intrinsic(v, o, 0, attacking_hoop(v, c, 0));
-#pragma unroll
-            for (int q = 0; q < INTRINSIC; q++) mine.v[q] = o.v[q];
-        }
-        lane_gather_view<N>(mine, slot);
-#pragma unroll
-        for (int t = 0; t < N; t++)
-#pragma unroll
-            for (int q = 0; q < INTRINSIC; q++) sh.intr[t].v[q] = slot[t].v[q];
-#pragma unroll
-        for (int t = 1; t < N; t++) {
-            const F3 to = v.pos(t) - v.pos(0);
-            const float l2 = len2(to);
-            const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
-            sh.rdir[0][t] = l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f);
-            sh.rlen[0][t] = bbm::sqrtf_(l2);
-        }
+        World<N> s;
+        load_world(s, p, w);
+        agent_view(s, v, lane % N);
+        load_words<6 * N>(r.actions, w, a_next);
     }
-    float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
-    const bool fast = active && canonical_slots(v, 0);
-    if constexpr (MODE == MODE_DIRECT_OBS) {
+    const double *erf_tab = erf_table_lds();
+    // Everything loaded so far has arrived before the loop: no register
+    // enters it with a load pending (which would make the compiler wait for
+    // the vector-memory counter inside every step).
+#if !defined(BB_RO_NO_PREWAIT)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
+    for (int t = 0; t < r.steps; t++) {
+        // Opaque per-step copies of the lane and world index: what derives
+        // from them (column addresses, agent ids, the tile flush's per-piece
+        // offsets) is recomputed each step instead of being hoisted out of the
+        // loop (or shared with the load before it) and held in registers --
+        // or spilled -- across it.  A spill reload is a memory load, and one
+        // issued after a step's stores waits for all of them.
+        int lane_t = lane;
+        int64_t w_t = w;
+        __asm__ volatile("" : "+v"(lane_t));
+        __asm__ volatile("" : "+v"(w_t));
+        const int k = lane_t % N;
+        const int64_t row = w_t * N + k;
+        Ctx c = make_ctx(p, w_t, k == 0);
+        c.erf_tab = erf_tab;
+        const LaneAgents<N, MODE_FULL> ag{k, &p};
+        int32_t *act_t = r.actions + (int64_t)t * rows * 6;
+        uint32_t *park = (uint32_t *)(tile + lane_t * T::RS);  // idle until the observation pass
+        int32_t ib = -1;
+        bool share = false;
         if (active) {
-            if (share) {
-                RowSink o;
-                o.row = grow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
-                emit_row_shared(v, c, sh, 0, o, ib);
-            } else if (fast) {
-                fill_obs_fast(v, c, 0, grow, ib);
-            } else {
-                fill_obs_slow(v, c, 0, grow, ib);
+            World<N> s;
+            agent_view<N, true>(v, s, k);
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) s.act[i][q] = (int32_t)a_next[6 * i + q];
+#pragma unroll
+            for (int q = 0; q < 6; q++) park[q] = (uint32_t)pick_by<N>(k, [&](int j) { return s.act[j][q]; });
+            // (unconditional -- the last step re-reads its own rows -- so that
+            // every path through the loop has the same loads in flight)
+            load_words<6 * N>(t + 1 < r.steps ? act_t + rows * 6 : act_t, w_t, a_next);
+#if !defined(BB_RO_NO_SYS)
+            step_world_pre_obs(s, c, ag);
+#endif
+            // Retire the prefetch here, before this step's stores are issued:
+            // waiting for it then waits only for what was issued before it
+            // (the previous step's stores, drained during these systems).  At
+            // the top of the next step the rows are already in registers.
+#pragma unroll
+            for (int q = 0; q < 6 * N; q++) __asm__ volatile("" : "+v"(a_next[q]));
+            ib = inbounder_id(s);
+            share = obs_sharable(s);
+            agent_view(s, v, k);
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
+            r.done[(int64_t)t * r.rd_step + row] = v.done[0];
+            // the defence AI's overrides go back into the staged rows
+            bool changed = false;
+#pragma unroll
+            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q];
+            if (changed) {
+                uint32_t a[6];
+#pragma unroll
+                for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
+                store_words<6>(act_t, row, a);
             }
         }
-    } else {
-        if (active && !fast) fill_obs_slow(v, c, 0, grow, ib);
-        obs_phases<N, MODE>(v, c, sh, share, fast, tile, w0 * N, lane, ib);
+        __syncthreads();  // parked rows read before the tile is rewritten
+#if !defined(BB_RO_NO_OBS)
+        agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane_t, w0, w_t, active, tile,
+                                        r.obs + (int64_t)t * r.obs_step);
+#endif
+        __syncthreads();  // the tile is rewritten by the next step
     }
-    trace_point<MODE>(p, 9);
+    if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
+        int64_t w_s = w;
+        __asm__ volatile("" : "+v"(w_s));
+        const int k = lane % N;
+        store_world_agent(v, p, w_s * N + k, 0);
+        if (k == 0) store_world_shared(v, p, w_s);  // world fields are not permuted in a view
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const RolloutArgs r)
+{
+    if constexpr (FusedRollout<N>::value) {
+        __shared__ float4 tile4[RolloutTile<N>::FLOATS / 4];
+        rollout_agent_lanes<N>(p, r, (float *)tile4);
+    }
 }
 
 // ------------------------------------------------------------------ N >= 4
@@ -669,6 +839,19 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 }
 
 template <int N>
+hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
+{
+    if constexpr (!FusedRollout<N>::value) {
+        return hipErrorNotSupported;
+    } else {
+        constexpr int WPB = Lanes<N>::WPB;
+        const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+        hipExtLaunchKernelGGL(k_rollout<N>, grid, block, 0, s, ev0, ev1, 0, p, r);
+        return hipGetLastError();
+    }
+}
+
+template <int N>
 hipError_t launch_init_t(const Params &p, hipStream_t s)
 {
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_init<N>), dim3((unsigned)((p.num_worlds + 255) / 256)), dim3(256), 0, s, p);
@@ -677,6 +860,8 @@ hipError_t launch_init_t(const Params &p, hipStream_t s)
 
 template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
+template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
+template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value; }
 template <> int step_grid<BB_N>(int64_t num_worlds) { return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB); }
 
 }  // namespace bb

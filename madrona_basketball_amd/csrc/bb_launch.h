@@ -18,14 +18,31 @@ enum StepMode : int {
     MODE_TRACE = 6,       // full, plus per-wave phase clocks into Params::diag_ts
 };
 
+// K-step rollout (bb_rollout): step t reads actions + t*W*N*6 and writes its
+// observation rows, rewards and done flags at obs/reward/done + t*(row stride).
+struct RolloutArgs {
+    int32_t *actions;  // [K][W][N][6]   (defence overrides written back)
+    float *obs;        // [K][W][N][OBSW]
+    float *reward;     // [K][W][N]
+    float *done;       // [K][W][N]
+    int64_t obs_step;  // floats between consecutive steps' obs (0: one buffer for all steps)
+    int64_t rd_step;   // floats between consecutive steps' reward/done (0: likewise)
+    int32_t steps;     // K
+};
+
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
 template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)
+template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
+                                             hipEvent_t ev1);
+template <int N> bool fused_rollout();  // k_rollout<N> exists (else: one k_step launch per step)
 
 #define BB_EXTERN_N(n)                                                                  \
     extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t); \
     extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);           \
-    template <> int step_grid<n>(int64_t);
+    template <> int step_grid<n>(int64_t);                                              \
+    extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
+    template <> bool fused_rollout<n>();
 BB_EXTERN_N(2)
 BB_EXTERN_N(4)
 BB_EXTERN_N(6)
@@ -36,6 +53,9 @@ BB_EXTERN_N(10)
 hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL, hipEvent_t ev0 = nullptr,
                        hipEvent_t ev1 = nullptr);
 hipError_t launch_init(int n, const Params &p, hipStream_t s);
+hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
+                          hipEvent_t ev1 = nullptr);
+bool fused_rollout_n(int n);
 int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);

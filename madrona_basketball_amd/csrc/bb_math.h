@@ -266,7 +266,9 @@ static constexpr double ERF_TAYLOR[13][17] = {
 // value there is > 0.7); 1 from 4 on, where erfc < 2^-25 and the float result
 // is 1.  Absolute error ~2e-16 (the reference rounds erf to float,
 // src/game.cpp:808).
-BB_HD double erf_d(double x)
+// tab: ERF_TAYLOR's 13 x 17 coefficients (the kernels pass a copy in LDS: a
+// per-lane table read there is an LDS read, not a memory load).
+BB_HD double erf_d(double x, const double *tab = &ERF_TAYLOR[0][0])
 {
     if (isnan_d(x)) return x;
     const double ax = fabs_d(x);
@@ -281,7 +283,7 @@ BB_HD double erf_d(double x)
     } else if (ax < 4.0) {
         const int k = (int)((ax - 0.75) * 4.0);
         const double t = ax - (0.875 + 0.25 * (double)k);  // exact, |t| <= 1/8
-        const double *a = ERF_TAYLOR[k];
+        const double *a = tab + k * (ERF_TD + 1);
         double p = a[ERF_TD];
 #pragma unroll
         for (int n = ERF_TD - 1; n >= 0; n--) p = fma_d(p, t, a[n]);

@@ -193,6 +193,13 @@ BB_HD constexpr int view_source(int slot, int k)
     return slot == 0 ? k : ((slot - 1) < k ? slot - 1 : slot);
 }
 
+// Slot of agent i in agent k's view (the inverse of view_source).
+template <int N>
+BB_HD constexpr int view_slot(int i, int k)
+{
+    return i == k ? 0 : (i < k ? i + 1 : i);
+}
+
 // From this agent count on the GPU kernel keeps the world in LDS
 // (bb_kernels.hip, Lanes::SHARED), where an indexed access is one LDS load.
 constexpr int LDS_WORLD_MIN_N = 4;
@@ -415,11 +422,12 @@ struct Ctx {
     const Params *p;
     int64_t w;
     bool writer;   // this lane performs the world's memory side effects
+    const double *erf_tab;  // bbm::ERF_TAYLOR (the GPU kernels: its copy in LDS)
 };
 
 BB_HD Ctx make_ctx(const Params &p, int64_t w, bool writer = true)
 {
-    Ctx c; c.p = &p; c.w = w; c.writer = writer; return c;
+    Ctx c; c.p = &p; c.w = w; c.writer = writer; c.erf_tab = &bbm::ERF_TAYLOR[0][0]; return c;
 }
 
 // sampleUniform at stream position ctr of the world's stream
@@ -950,7 +958,7 @@ BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
     const float vs = VEL_DEV * len(pick_by<N>(i, [&](int j) { return s.vel(j); }));
     const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
     const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
-    return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)));
+    return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)), c.erf_tab);
 }
 
 template <int N, class A>
@@ -1683,13 +1691,14 @@ BB_HD T pick(const T (&a)[N], int idx)
 }
 
 
-template <int N>
+// INV: the inverse map -- v from agent k's view back to creation order.
+template <int N, bool INV = false>
 BB_HD void agent_view(const World<N> &s, World<N> &v, int k)
 {
     v = s;
 #pragma unroll
     for (int j = 0; j < N; j++) {
-        const int src = view_source<N>(j, k);
+        const int src = INV ? view_slot<N>(j, k) : view_source<N>(j, k);
 #define BB_V(f) v.f[j] = pick(s.f, src);
         BB_V(rst) BB_V(cd) BB_V(px) BB_V(py) BB_V(pz) BB_V(rew) BB_V(done) BB_V(step)
         BB_V(has) BB_V(bid) BB_V(pw) BB_V(qw) BB_V(qx) BB_V(qy) BB_V(qz) BB_V(inb) BB_V(allow)

@@ -216,6 +216,51 @@ class SimpleGridworldSimulator:
                                                 ctypes.byref(ms) if time_kernels else None), "step_n_staged")
         return ms.value if time_kernels else None
 
+    def rollout_buffers(self, n: int) -> dict:
+        """Zeroed [n, W, N, ...] outputs for rollout() on the sim's device:
+        obs float32 [n, W, N, OBSW], reward / done float32 [n, W, N] (the
+        storage of scripts/ppo.py:63-70's rollout buffers)."""
+        W, N = self._num_worlds, self._num_agents
+        ow = self._views["observations"].shape[-1]
+        return {
+            "obs": torch.zeros((n, W, N, ow), dtype=torch.float32, device=self._device),
+            "reward": torch.zeros((n, W, N), dtype=torch.float32, device=self._device),
+            "done": torch.zeros((n, W, N), dtype=torch.float32, device=self._device),
+        }
+
+    def rollout(self, actions: torch.Tensor, obs: torch.Tensor = None, reward: torch.Tensor = None,
+                done: torch.Tensor = None, per_step: bool = False, time_kernels: bool = False):
+        """len(actions) steps in one native call (bb_rollout): step k takes
+        actions[k] ([W, N, 6] int32; the defence AI's overrides are written
+        back) and its observations / rewards / done flags land in obs[k],
+        reward[k], done[k] (rollout_buffers(); None: not recorded).  One
+        launch for all steps on gfx950 at 2 agents (worlds held in registers);
+        per_step=True forces one step launch per step.  Afterwards every
+        tensor of the simulator holds the state after the last step."""
+        n = actions.shape[0]
+        W, N = self._num_worlds, self._num_agents
+        ow = self._views["observations"].shape[-1]
+
+        def ok(t, shape, dtype):
+            return (t is None or (tuple(t.shape) == shape and t.dtype == dtype and t.is_contiguous()
+                                  and t.device == self._device))
+        if not ok(actions, (n, W, N, 6), torch.int32):
+            raise ValueError("actions must be a contiguous int32 [n, num_worlds, num_agents, 6] tensor "
+                             "on the simulator's device")
+        if not (ok(obs, (n, W, N, ow), torch.float32) and ok(reward, (n, W, N), torch.float32)
+                and ok(done, (n, W, N), torch.float32)):
+            raise ValueError("rollout outputs must be contiguous float32 tensors shaped like rollout_buffers(n)")
+        if (reward is None) != (done is None):
+            raise ValueError("reward and done are recorded together")
+
+        def ptr(t):
+            return ctypes.c_void_p(None if t is None else t.data_ptr())
+        ms = ctypes.c_float(0.0)
+        _lib.check(_lib.load().bb_rollout(self._h, int(n), ptr(actions), ptr(obs), ptr(reward), ptr(done),
+                                          _lib.ROLLOUT_PER_STEP if per_step else 0, self._stream(),
+                                          ctypes.byref(ms) if time_kernels else None), "rollout")
+        return ms.value if time_kernels else None
+
     def write_random_actions(self, action_seed: int, step: int) -> None:
         _lib.check(_lib.load().bb_write_random_actions(self._h, int(action_seed) & 0xFFFFFFFF,
                                                        int(step) & 0xFFFFFFFF, self._stream()),

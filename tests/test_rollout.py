@@ -1,0 +1,225 @@
+"""K-step rollouts (bb_rollout).
+
+bb_rollout(actions[K]) must leave exactly what K times
+(action tensor := actions[k]; step(); record observations / reward / done)
+leaves -- recorded outputs, the defence AI's overrides written back into
+actions[k], and every simulator column afterwards -- bit for bit, on the host
+executor, the per-step GPU path and the fused gfx950 kernel (one launch, the
+worlds held in registers).  The oracle (test infrastructure) checks the
+recorded per-step outputs directly.
+"""
+import numpy as np
+import pytest
+import torch
+
+from madrona_basketball_amd import ExecMode
+from oracle.oracle import Oracle
+from tests.helpers import compare, make_sim, oracle_flags
+
+
+def stepwise_reference(sim, actions):
+    """The loop bb_rollout replaces: per step, the staged actions then one step;
+    returns (obs, reward, done, actions as written back)."""
+    acts = actions.clone()
+    obs, rew, done = [], [], []
+    for k in range(acts.shape[0]):
+        sim.step_n_staged(acts[k:k + 1])
+        obs.append(sim.observations_tensor().to_torch().clone())
+        rew.append(sim.reward_tensor().to_torch().clone())
+        done.append(sim.done_tensor().to_torch().clone())
+    return torch.stack(obs), torch.stack(rew), torch.stack(done), acts
+
+
+def assert_same(a, b, what):
+    assert a.shape == b.shape and a.dtype == b.dtype, what
+    assert torch.equal(a.contiguous().view(torch.int32).cpu(), b.contiguous().view(torch.int32).cpu()), what
+
+
+def assert_same_sims(a, b):
+    for name in a._views:
+        assert_same(a._views[name], b._views[name], name)
+
+
+@pytest.mark.parametrize("num_agents", [2, 4])
+def test_host_rollout_equals_stepwise(num_agents):
+    W, K = 96, 70
+    a = make_sim(ExecMode.CPU, W, num_agents=num_agents, per_world_rng=True)
+    b = make_sim(ExecMode.CPU, W, num_agents=num_agents, per_world_rng=True)
+    acts = a.stage_random_actions(K, action_seed=321, step0=0)
+    buf = a.rollout_buffers(K)
+    a_acts = acts.clone()
+    a.rollout(a_acts, buf["obs"], buf["reward"], buf["done"])
+    obs, rew, done, b_acts = stepwise_reference(b, acts)
+    assert_same(buf["obs"], obs, "obs")
+    assert_same(buf["reward"], rew, "reward")
+    assert_same(buf["done"], done, "done")
+    assert_same(a_acts, b_acts, "actions written back")
+    assert_same_sims(a, b)
+
+
+def test_host_rollout_outputs_match_oracle_every_step():
+    W, K = 64, 160
+    sim = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    o = Oracle(W, flags=oracle_flags(per_world_rng=True))
+    acts = sim.stage_random_actions(K, action_seed=5, step0=0)
+    buf = sim.rollout_buffers(K)
+    staged = acts.clone()
+    sim.rollout(staged, buf["obs"], buf["reward"], buf["done"])
+    for k in range(K):
+        o.random_actions(5, k)
+        o.step()
+        for name, got in (("observations", buf["obs"][k]), ("reward", buf["reward"][k]), ("done", buf["done"][k])):
+            exp = o.export(name)
+            g = got.numpy()
+            if name == "done":
+                assert np.array_equal(g, exp), (k, name)
+            else:
+                assert np.allclose(g, exp, atol=1e-5, rtol=1e-6), (k, name)
+        assert np.array_equal(staged[k].numpy(), o.export("action")), (k, "action written back")
+    bad, _ = compare(sim, o)
+    assert not bad, bad
+
+
+def test_host_rollout_unrecorded_outputs_and_chunks():
+    """NULL outputs rewrite the simulator's tensors each step; two chunks of a
+    rollout == one rollout over both."""
+    W, K = 40, 50
+    a = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    b = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    acts = a.stage_random_actions(2 * K, action_seed=9, step0=0)
+    a.rollout(acts[:K].clone())
+    a.rollout(acts[K:].clone())
+    buf = b.rollout_buffers(2 * K)
+    b.rollout(acts.clone(), buf["obs"], buf["reward"], buf["done"])
+    assert_same_sims(a, b)
+
+
+def test_rollout_argument_errors():
+    sim = make_sim(ExecMode.CPU, 8)
+    acts = sim.stage_random_actions(3)
+    buf = sim.rollout_buffers(3)
+    with pytest.raises(ValueError):
+        sim.rollout(acts[:, :4].contiguous())
+    with pytest.raises(ValueError):
+        sim.rollout(acts, buf["obs"][:, :, :, :64].contiguous())
+    with pytest.raises(ValueError):
+        sim.rollout(acts, reward=buf["reward"])
+    sim.rollout(acts[:0].contiguous())  # zero steps: nothing happens
+
+
+# ------------------------------------------------------------------ GPU
+def _gpu():
+    assert torch.cuda.is_available(), "GPU tests selected but no HIP device is visible"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [dict(), dict(tag_mask=False), dict(one_on_one=False, tag_mask=False)])
+def test_gpu_fused_rollout_equals_per_step_and_host(native_lib, flags):
+    """Fused k_rollout<2> == per-step launches == host executor, bit for bit.
+    8190 worlds: the last wave is partly filled."""
+    _gpu()
+    W, K = 8190, 96
+    f = make_sim(ExecMode.CUDA, W, per_world_rng=True, **flags)
+    p = make_sim(ExecMode.CUDA, W, per_world_rng=True, **flags)
+    h = make_sim(ExecMode.CPU, W, per_world_rng=True, **flags)
+    acts = f.stage_random_actions(K, action_seed=321, step0=0)
+    outs = {}
+    for name, sim, per_step in (("fused", f, False), ("per_step", p, True), ("host", h, False)):
+        a = acts.clone() if sim is not h else acts.cpu().clone()
+        buf = sim.rollout_buffers(K)
+        sim.rollout(a, buf["obs"], buf["reward"], buf["done"], per_step=per_step)
+        outs[name] = (a, buf)
+    torch.cuda.synchronize()
+    for other in ("per_step", "host"):
+        assert_same(outs["fused"][0], outs[other][0], f"actions vs {other}")
+        for key in ("obs", "reward", "done"):
+            assert_same(outs["fused"][1][key], outs[other][1][key], f"{key} vs {other}")
+    assert_same_sims(f, p)
+    assert_same_sims(f, h)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_rollout_matches_oracle_per_step(native_lib, oracle_lib):
+    _gpu()
+    W, K = 2048, 300
+    sim = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    o = Oracle(W, flags=oracle_flags(per_world_rng=True))
+    acts = sim.stage_random_actions(K, action_seed=77, step0=0)
+    buf = sim.rollout_buffers(K)
+    sim.rollout(acts, buf["obs"], buf["reward"], buf["done"])
+    torch.cuda.synchronize()
+    obs, rew, done, acts = (t.cpu().numpy() for t in (buf["obs"], buf["reward"], buf["done"], acts))
+    for k in range(K):
+        o.random_actions(77, k)
+        o.step()
+        assert np.array_equal(done[k], o.export("done")), k
+        assert np.allclose(rew[k], o.export("reward"), atol=1e-5, rtol=1e-6), k
+        assert np.allclose(obs[k], o.export("observations"), atol=1e-5, rtol=1e-6), k
+        assert np.array_equal(acts[k], o.export("action")), k
+    bad, _ = compare(sim, o)
+    assert not bad, bad
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_chunks_and_unrecorded(native_lib):
+    """Chunked fused rollouts (and unrecorded outputs) == one long rollout;
+    the observation tail columns stay zero."""
+    _gpu()
+    W, K = 4096, 40
+    a = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    b = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    acts = a.stage_random_actions(3 * K, action_seed=3, step0=0)
+    a.rollout(acts[:K].clone())
+    bufa = a.rollout_buffers(K)
+    a.rollout(acts[K:2 * K].clone(), bufa["obs"], bufa["reward"], bufa["done"])
+    a.rollout(acts[2 * K:].clone())
+    bufb = b.rollout_buffers(3 * K)
+    b.rollout(acts.clone(), bufb["obs"], bufb["reward"], bufb["done"])
+    torch.cuda.synchronize()
+    assert_same_sims(a, b)
+    for key in ("obs", "reward", "done"):
+        assert_same(bufa[key], bufb[key][K:2 * K], key)
+    used = (61 + 38 + 4 + 3) // 4 * 4
+    assert int(torch.count_nonzero(bufb["obs"][..., used:])) == 0
+    assert int(torch.count_nonzero(b.observations_tensor().to_torch()[..., used:])) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_more_agents_per_step_path(native_lib):
+    """N = 4 has no fused kernel: bb_rollout launches k_step per step."""
+    _gpu()
+    W, K = 700, 60
+    g = make_sim(ExecMode.CUDA, W, num_agents=4, per_world_rng=True)
+    h = make_sim(ExecMode.CPU, W, num_agents=4, per_world_rng=True)
+    acts = g.stage_random_actions(K, action_seed=4, step0=0)
+    bg, bh = g.rollout_buffers(K), h.rollout_buffers(K)
+    ag, ah = acts.clone(), acts.cpu().clone()
+    g.rollout(ag, bg["obs"], bg["reward"], bg["done"])
+    h.rollout(ah, bh["obs"], bh["reward"], bh["done"])
+    torch.cuda.synchronize()
+    assert_same(ag, ah, "actions")
+    for key in ("obs", "reward", "done"):
+        assert_same(bg[key], bh[key], key)
+    assert_same_sims(g, h)
+
+
+@pytest.mark.gpu
+def test_gpu_fused_rollout_full_size_identical_worlds(native_lib):
+    """65 536 worlds, shared RNG key, identical actions in every world: every
+    recorded step and the final state stay identical across worlds."""
+    _gpu()
+    W, K = 65536, 128
+    sim = make_sim(ExecMode.CUDA, W)
+    gen = np.random.default_rng(8)
+    a = np.stack([gen.integers(0, b, size=(K, 2)) for b in (2, 8, 3, 2, 2, 2)], axis=-1).astype(np.int32)
+    acts = torch.from_numpy(a)[:, None].expand(K, W, 2, 6).contiguous().cuda()
+    buf = sim.rollout_buffers(K)
+    sim.rollout(acts, buf["obs"], buf["reward"], buf["done"])
+    torch.cuda.synchronize()
+    for key in ("obs", "reward", "done"):
+        v = buf[key].view(torch.int32)
+        assert torch.equal(v, v[:, :1].expand_as(v)), key
+    assert torch.equal(acts, acts[:, :1].expand_as(acts))
+    for name, v in sim._views.items():
+        flat = v.reshape(W, -1).view(torch.int32) if v.dim() > 1 else v.view(torch.int32)[:, None]
+        assert torch.equal(flat, flat[:1].expand_as(flat)), name

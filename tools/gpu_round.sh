@@ -43,6 +43,12 @@ for s in $STEPS; do
     smoke) run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rA ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 100 ;;
+    rtests) run pytest_rollout 600 python -u -m pytest tests/test_rollout.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    benchr:*) k=${s#benchr:}; run "bench_r$k" 600 python bench.py --steps 1024 --warmup 64 --rollout $k --no-cpu-baseline ;;
+    profr:*) k=${s#profr:}
+        ( cd /tmp && export TMPDIR=/tmp && run "prof_r$k" 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r$k" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps 512 --warmup 32 --rollout $k --no-cpu-baseline ) || exit $?
+        ;;
     bench262k) run bench262k 600 python bench.py --worlds 262144 --steps 300 --warmup 50 --no-cpu-baseline ;;
     bench8k) run bench8k 600 python bench.py --worlds 8192 --steps 1000 --warmup 100 --no-cpu-baseline ;;
     bench4) run bench4 600 python bench.py --agents 4 --steps 300 --warmup 50 --no-cpu-baseline ;;
