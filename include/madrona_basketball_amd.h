@@ -18,6 +18,9 @@
  *   bb_rollout          <- n x (actions[:] = a_k; Manager::step; copy of
  *                          observations/rewards/dones), the rollout loop of
  *                          scripts/ppo.py:139-176 with a_k staged in HBM
+ *   bb_record           <- the per-step trajectory logging of scripts/ppo.py:93-106
+ *                          and scripts/infer.py:116-129 (ten .cpu() copies per
+ *                          step), as one device-side copy into a ring
  *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
  *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
  *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
@@ -183,6 +186,17 @@ int bb_fill_random_actions(bb_sim *sim, int32_t *actions, int32_t n, uint32_t ac
  * kernel_ms as in bb_step_n (summed over the launches). */
 int bb_rollout(bb_sim *sim, int32_t n, int32_t *actions, float *obs_out, float *reward_out, float *done_out,
                uint32_t flags, void *stream, float *kernel_ms);
+
+/* Trajectory recorder.  One record of one world is bb_record_words(N) int32
+ * words (18 N + 27): the columns scripts/ppo.py:94-105 logs, in its key order
+ * and each in its export layout -- agent_pos f32[N][3], ball_pos f32[3],
+ * ball_vel f32[3], orientation f32[N][4], ball_physics i32[7],
+ * agent_possession i32[N][3], game_state f32[14], reward f32[N],
+ * action i32[N][6], done f32[N].  bb_record copies worlds [world0,
+ * world0 + count) to dst + slot * count * words (records world-major), on
+ * `stream` after whatever precedes it there; host memory in CPU mode. */
+int32_t bb_record_words(int32_t num_agents);
+int bb_record(bb_sim *sim, int64_t world0, int32_t count, int32_t *dst, int64_t slot, void *stream);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

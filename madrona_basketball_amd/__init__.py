@@ -7,6 +7,8 @@ step kernel (csrc/bb_kernels.hip) and a host executor for ExecMode.CPU.
 from . import madrona
 from .madrona import ExecMode
 from .simulator import SimpleGridworldSimulator, Tensor
+from .recorder import TrajectoryRecorder
 from ._lib import ABI_SYMBOLS, EXPORT_IDS
 
-__all__ = ["SimpleGridworldSimulator", "Tensor", "ExecMode", "madrona", "ABI_SYMBOLS", "EXPORT_IDS"]
+__all__ = ["SimpleGridworldSimulator", "Tensor", "TrajectoryRecorder", "ExecMode", "madrona", "ABI_SYMBOLS",
+           "EXPORT_IDS"]

@@ -42,6 +42,7 @@ ABI_SYMBOLS = [
     "bb_default_config", "bb_obs_width", "bb_buffer_bytes", "bb_create",
     "bb_create_with_buffers", "bb_destroy", "bb_step", "bb_step_n",
     "bb_write_random_actions", "bb_step_n_staged", "bb_fill_random_actions", "bb_rollout",
+    "bb_record_words", "bb_record",
     "bb_set_action", "bb_trigger_reset", "bb_export",
     "bb_num_worlds", "bb_num_agents", "bb_exec_mode", "bb_algorithmic_bytes_per_world",
     "bb_rollout_fused", "bb_rollout_bytes_per_world_step", "bb_rollout_state_bytes_per_world",
@@ -95,6 +96,8 @@ def load():
         "bb_step_n_staged": (ctypes.c_int, [vp, i32, vp, vp, ctypes.POINTER(ctypes.c_float)]),
         "bb_fill_random_actions": (ctypes.c_int, [vp, vp, i32, u32, u32, vp]),
         "bb_rollout": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, u32, vp, ctypes.POINTER(ctypes.c_float)]),
+        "bb_record_words": (i32, [i32]),
+        "bb_record": (ctypes.c_int, [vp, i64, i32, vp, i64, vp]),
         "bb_set_action": (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "bb_trigger_reset": (ctypes.c_int, [vp, i32, vp]),
         "bb_export": (ctypes.c_int, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(i32),

@@ -32,6 +32,58 @@ __global__ void k_poke(int32_t *dst, int32_t count, Poke vals)
     if (k < count) dst[k] = vals.v[k];
 }
 
+// Trajectory recorder: one lane per record word; consecutive lanes write
+// consecutive words of the ring slot (the source reads are the scattered side,
+// a few hundred bytes per world).
+int32_t record_words(int n) { return 18 * n + 27; }
+
+RecordArgs record_args(const Params &p, int n)
+{
+    const Columns &c = p.c;
+    RecordArgs a;
+    const void *src[RECORD_SEGS] = {c.agent_pos, c.ball_pos, c.ball_vel, c.orientation, c.ball_physics,
+                                    c.possession, c.game_state, c.reward, c.action, c.done};
+    const int32_t wpw[RECORD_SEGS] = {3 * n, 3, 3, 4 * n, 7, 3 * n, 14, n, 6 * n, n};
+    a.off[0] = 0;
+    for (int k = 0; k < RECORD_SEGS; k++) {
+        a.src[k] = (const uint32_t *)src[k];
+        a.wpw[k] = wpw[k];
+        a.off[k + 1] = a.off[k] + wpw[k];
+    }
+    return a;
+}
+
+__host__ __device__ inline uint32_t record_word(const RecordArgs &a, int64_t world, int32_t q)
+{
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < RECORD_SEGS; j++) k += q >= a.off[j] ? 1 : 0;
+    // (select chain: a per-lane index into the kernel-argument arrays stays in scalars)
+    const uint32_t *src = a.src[0];
+    int32_t wpw = a.wpw[0], off = a.off[0];
+#pragma unroll
+    for (int j = 1; j < RECORD_SEGS; j++) {
+        if (k == j) { src = a.src[j]; wpw = a.wpw[j]; off = a.off[j]; }
+    }
+    return src[world * wpw + (q - off)];
+}
+
+__global__ __launch_bounds__(256) void k_record(const RecordArgs a, int64_t world0, int64_t total, uint32_t *dst)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= total) return;
+    const int32_t words = a.off[RECORD_SEGS];
+    const int64_t wl = i / words;
+    dst[i] = record_word(a, world0 + wl, (int32_t)(i - wl * words));
+}
+
+void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst)
+{
+    const int32_t words = a.off[RECORD_SEGS];
+    for (int64_t wl = 0; wl < count; wl++)
+        for (int32_t q = 0; q < words; q++) dst[wl * words + q] = record_word(a, world0 + wl, q);
+}
+
 // Coalesced streaming probe: item i reads read_q float4 and writes write_q
 // float4, laid out [q][item] so every wave instruction is 1 KiB contiguous.
 __global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q)
@@ -64,6 +116,14 @@ hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t
     Poke pk;
     for (int k = 0; k < 16; k++) pk.v[k] = k < count ? vals[k] : 0;
     hipLaunchKernelGGL(k_poke, dim3(1), dim3(64), 0, s, dst, count, pk);
+    return hipGetLastError();
+}
+
+hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s)
+{
+    const int64_t total = (int64_t)count * a.off[RECORD_SEGS];
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_record, grid_for(total, 256), dim3(256), 0, s, a, world0, total, dst);
     return hipGetLastError();
 }
 

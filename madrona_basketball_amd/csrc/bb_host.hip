@@ -658,6 +658,26 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
     return BB_OK;
 }
 
+int32_t bb_record_words(int32_t n) { return bb::record_words(n); }
+
+int bb_record(bb_sim *s, int64_t world0, int32_t count, int32_t *dst, int64_t slot, void *stream)
+{
+    if (!s || !dst || count < 0 || slot < 0) return fail(BB_ERR_INVALID_ARG, "bb_record");
+    if (world0 < 0 || world0 + count > s->cfg.num_worlds)
+        return fail(BB_ERR_INVALID_ARG, "bb_record: worlds [" + std::to_string(world0) + ", " +
+                                            std::to_string(world0 + count) + ") outside the simulator");
+    const bb::RecordArgs a = bb::record_args(s->p, s->n);
+    uint32_t *d = (uint32_t *)dst + slot * (int64_t)count * bb::record_words(s->n);
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) {
+        bb::host_record(a, world0, count, d);
+        return BB_OK;
+    }
+    DeviceGuard g(s->device);
+    hipError_t e = bb::launch_record(a, world0, count, d, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "launch record kernel");
+    return BB_OK;
+}
+
 int bb_set_action(bb_sim *s, int32_t world_idx, int32_t agent_idx, int32_t move_speed, int32_t move_angle,
                   int32_t rotate, int32_t grab, int32_t pass, int32_t shoot, void *stream)
 {

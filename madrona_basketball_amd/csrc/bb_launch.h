@@ -30,6 +30,16 @@ struct RolloutArgs {
     int32_t steps;     // K
 };
 
+// Trajectory recorder (bb_record): NSEG column segments per recorded world.
+constexpr int RECORD_SEGS = 10;
+struct RecordArgs {
+    const uint32_t *src[RECORD_SEGS];  // column bases
+    int32_t wpw[RECORD_SEGS];          // words per world of each column
+    int32_t off[RECORD_SEGS + 1];      // word offset of each segment in a record
+};
+int32_t record_words(int n);
+RecordArgs record_args(const Params &p, int n);
+
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
 template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)
@@ -59,6 +69,8 @@ bool fused_rollout_n(int n);
 int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);
+hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s);
+void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)
 hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, hipStream_t s);
 

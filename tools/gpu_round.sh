@@ -43,6 +43,15 @@ for s in $STEPS; do
     smoke) run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rA ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 100 ;;
+    rectests) run pytest_recorder 600 python -u -m pytest tests/test_recorder.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
+    pmcr:*) k=${s#pmcr:}
+        ( cd /tmp && export TMPDIR=/tmp && run "pmcr${k}_fetch" 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcr${k}_fetch" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps $((4*k)) --warmup $k --rollout $k --no-cpu-baseline ) || exit $?
+        ( cd /tmp && export TMPDIR=/tmp && run "pmcr${k}_write" 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcr${k}_write" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps $((4*k)) --warmup $k --rollout $k --no-cpu-baseline ) || exit $?
+        python3 tools/traffic.py "$OUT/pmcr${k}_fetch" "$OUT/pmcr${k}_write" W65536_N2_R$k --kernel "k_rollout<2>" \
+            --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
+        ;;
     rtests) run pytest_rollout 600 python -u -m pytest tests/test_rollout.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     benchr:*) k=${s#benchr:}; run "bench_r$k" 600 python bench.py --steps 1024 --warmup 64 --rollout $k --no-cpu-baseline ;;
     profr:*) k=${s#profr:}
