@@ -21,6 +21,9 @@
  *   bb_record           <- the per-step trajectory logging of scripts/ppo.py:93-106
  *                          and scripts/infer.py:116-129 (ten .cpu() copies per
  *                          step), as one device-side copy into a ring
+ *   bb_policy_forward   <- Agent.forward of scripts/agent.py:140-154 (32 channels,
+ *                          2 layers, env.py:107) + the action write of
+ *                          scripts/env.py:147, fused on the device
  *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
  *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
  *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
@@ -197,6 +200,28 @@ int bb_rollout(bb_sim *sim, int32_t n, int32_t *actions, float *obs_out, float *
  * `stream` after whatever precedes it there; host memory in CPU mode. */
 int32_t bb_record_words(int32_t num_agents);
 int bb_record(bb_sim *sim, int64_t world0, int32_t count, int32_t *dst, int64_t slot, void *stream);
+
+/* Policy inference (scripts/agent.py:108-154 at num_channels = 32,
+ * num_layers = 2, input 128, buckets [2,8,3,2,2,2]).  fp32 row-major
+ * [out][in] weights on the device (host memory for BB_EXEC_CPU); obs_inv =
+ * rsqrt(running var + 1e-5) as agent.py:30-35 computes it; head_w / head_b =
+ * the 19 actor rows, the critic row, then 12 zero rows (32 x 32, 32). */
+typedef struct bb_policy_weights {
+    const float *obs_mean, *obs_inv;
+    const float *w1, *b1, *ln1_w, *ln1_b;
+    const float *w2, *b2, *ln2_w, *ln2_b;
+    const float *head_w, *head_b;
+} bb_policy_weights;
+
+/* For rows r in [0, rows): reads obs + r * obs_stride (128 floats, 16-byte
+ * aligned), writes 6 int32 actions to actions + r * action_stride (e.g. the
+ * action tensor's column of one agent), and optionally log_prob[r] (sum over
+ * the buckets) and value[r].  stochastic = 0: per-bucket argmax (best(),
+ * scripts/action.py:21-23); 1: Gumbel-max sample keyed threefry({seed, step},
+ * {r, logit}).  gpu_id: the device of the pointers (CUDA mode). */
+int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu_id, const float *obs,
+                      int64_t rows, int64_t obs_stride, int32_t *actions, int64_t action_stride, float *log_prob,
+                      float *value, int32_t stochastic, uint32_t seed, uint32_t step, void *stream);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

@@ -21,9 +21,10 @@ KERNEL_FLAGS = ["-mllvm", "-disable-machine-licm"]
 # (source, extra flags, object name): the step kernel once per agent count,
 # compiled in parallel
 UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}", *KERNEL_FLAGS], f"bb_kernels_n{n}.o") for n in AGENT_COUNTS]
-         + [("bb_common.hip", [], "bb_common.o"), ("bb_host.hip", [], "bb_host.o")])
+         + [("bb_common.hip", [], "bb_common.o"), ("bb_host.hip", [], "bb_host.o"),
+            ("bb_policy.hip", [], "bb_policy.o")])
 SOURCES = sorted({u[0] for u in UNITS})
-HEADERS = ["bb_math.h", "bb_rng.h", "bb_sim.h", "bb_launch.h"]
+HEADERS = ["bb_math.h", "bb_rng.h", "bb_sim.h", "bb_launch.h", "bb_policy.h"]
 ARCH = os.environ.get("BB_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: every float op rounds on its own (bit parity host <-> gfx950)

@@ -658,6 +658,36 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
     return BB_OK;
 }
 
+int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu_id, const float *obs, int64_t rows,
+                      int64_t obs_stride, int32_t *actions, int64_t action_stride, float *log_prob, float *value,
+                      int32_t stochastic, uint32_t seed, uint32_t step, void *stream)
+{
+    if (!w || !obs || !actions || rows < 0 || obs_stride < bb::POL_IN || action_stride < 6)
+        return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: arguments");
+    const float *req[] = {w->obs_mean, w->obs_inv, w->w1, w->b1, w->ln1_w, w->ln1_b, w->w2, w->b2, w->ln2_w,
+                          w->ln2_b, w->head_w, w->head_b};
+    for (const float *ptr : req)
+        if (!ptr) return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: a weight pointer is NULL");
+    if ((((uintptr_t)obs) & 15u) || (obs_stride & 3) || (((uintptr_t)w->w1) & 15u))
+        return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: obs rows and w1 must be 16-byte aligned");
+    bb::PolicyArgs a;
+    a.w = bb::PolicyWeights{w->obs_mean, w->obs_inv, w->w1, w->b1, w->ln1_w, w->ln1_b,
+                            w->w2, w->b2, w->ln2_w, w->ln2_b, w->head_w, w->head_b};
+    a.obs = obs; a.obs_stride = obs_stride; a.rows = rows;
+    a.actions = actions; a.act_stride = action_stride;
+    a.log_prob = log_prob; a.value = value;
+    a.stochastic = stochastic ? 1 : 0; a.seed = seed; a.step = step;
+    if (exec_mode == BB_EXEC_CPU) {
+        bb::host_policy(a);
+        return BB_OK;
+    }
+    if (exec_mode != BB_EXEC_CUDA) return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: exec_mode");
+    DeviceGuard g(gpu_id);
+    hipError_t e = bb::launch_policy(a, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "launch policy kernel");
+    return BB_OK;
+}
+
 int32_t bb_record_words(int32_t n) { return bb::record_words(n); }
 
 int bb_record(bb_sim *s, int64_t world0, int32_t count, int32_t *dst, int64_t slot, void *stream)

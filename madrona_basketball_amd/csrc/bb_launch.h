@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "bb_sim.h"
+#include "bb_policy.h"
 
 namespace bb {
 
@@ -69,6 +70,8 @@ bool fused_rollout_n(int n);
 int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);
+hipError_t launch_policy(const PolicyArgs &a, hipStream_t s);
+void host_policy(const PolicyArgs &a);
 hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s);
 void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)

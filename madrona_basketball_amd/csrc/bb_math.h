@@ -227,6 +227,36 @@ BB_HD double exp_d(double x)
     return ldexp_d(p, (int)k);
 }
 
+// log (the policy's logsumexp and Gumbel noise, bb_policy.h): x = m 2^e with
+// m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m - 1)/(m + 1), |s| <= 0.1716:
+// odd series to s^25 (next term < 2^-60).
+BB_HD double log_d(double x)
+{
+    if (isnan_d(x) || x < 0.0) return nan_d();
+    if (x == 0.0) return -inf_d();
+    if (x == inf_d()) return x;
+    int e = 0;
+    double m = __builtin_frexp(x, &e);  // [0.5, 1)
+    if (m < 0.7071067811865476) { m = m * 2.0; e -= 1; }
+    const double s = (m - 1.0) / (m + 1.0);
+    const double z = s * s;
+    double p = 1.0 / 25.0;
+    p = fma_d(p, z, 1.0 / 23.0);
+    p = fma_d(p, z, 1.0 / 21.0);
+    p = fma_d(p, z, 1.0 / 19.0);
+    p = fma_d(p, z, 1.0 / 17.0);
+    p = fma_d(p, z, 1.0 / 15.0);
+    p = fma_d(p, z, 1.0 / 13.0);
+    p = fma_d(p, z, 1.0 / 11.0);
+    p = fma_d(p, z, 1.0 / 9.0);
+    p = fma_d(p, z, 1.0 / 7.0);
+    p = fma_d(p, z, 1.0 / 5.0);
+    p = fma_d(p, z, 1.0 / 3.0);
+    const double lm = 2.0 * fma_d(s * z, p, s);
+    const double k = (double)e;
+    return fma_d(k, LN2_HI, fma_d(k, LN2_LO, lm));
+}
+
 // Maclaurin coefficients of erf(x) sqrt(pi)/(2x) in z = x^2: (-1)^n / (n! (2n+1)),
 // folded at compile time (identical on host and device).
 static constexpr int ERF_NT = 17;  // z <= 0.5625: term 17 < 1e-19

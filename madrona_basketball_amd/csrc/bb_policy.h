@@ -1,0 +1,160 @@
+// bb_policy.h -- the reference's policy network (scripts/agent.py:108-154 with
+// num_channels = 32, num_layers = 2, env.py:107 / infer.py:182,203) for one
+// observation row, shared by the host executor and the gfx950 kernel
+// (bb_policy.hip) so that both give the same bits.
+//
+//   x  = clamp((obs - mean) * rsqrt(var + 1e-5), -5, 5)        RunningMeanStd, agent.py:28-38
+//   h1 = relu(LN(W1 x + b1)),  h2 = relu(LN(W2 h1 + b2))       backbone, agent.py:115-124
+//   logits = Wa h2 + ba (19),  value = Wc h2 + bc              heads, agent.py:127-128
+//   per bucket [2,8,3,2,2,2] (env.py:102): action = argmax (best(), action.py:21-23) or a
+//   Gumbel-max sample; log_prob = logit - logsumexp (Categorical, action.py:16-33), summed.
+//
+// Arithmetic order (fixed, -ffp-contract=off): each matrix product is the k-ordered
+// fmaf chain the gfx950 f32 MFMA computes (v_mfma_f32_16x16x4_f32: one rounding per
+// product), over the k permutation the kernel's operand layout gives -- k = 32q + j for
+// the 128-wide layer (j outer, q inner), k = 8q + j for the 32-wide ones; LayerNorm
+// sums are the kernel's butterfly tree.  exp / log: bb_math (correctly rounded floats).
+#pragma once
+#include "bb_math.h"
+#include "bb_rng.h"
+
+namespace bb {
+
+constexpr int POL_IN = 128;     // observation width read (obs row: agent.py input_dim)
+constexpr int POL_HID = 32;     // num_channels
+constexpr int POL_LOGITS = 19;  // sum of the buckets
+constexpr int POL_HEAD = 32;    // head rows: 19 actor + 1 critic + 12 zero
+constexpr int POL_BUCKETS = 6;
+BB_HD int pol_bucket(int b) { return b == 1 ? 8 : (b == 2 ? 3 : 2); }  // [2, 8, 3, 2, 2, 2]
+
+// Device (or host) pointers, fp32, row-major [out][in].
+struct PolicyWeights {
+    const float *obs_mean, *obs_inv;           // [128]: mean, rsqrt(var + eps) as torch computes it
+    const float *w1, *b1, *ln1_w, *ln1_b;      // [32][128], [32] x3
+    const float *w2, *b2, *ln2_w, *ln2_b;      // [32][32], [32] x3
+    const float *head_w, *head_b;              // [32][32], [32]
+};
+
+struct PolicyArgs {
+    PolicyWeights w;
+    const float *obs;      // row r at obs + r * obs_stride
+    int64_t obs_stride;    // floats
+    int64_t rows;
+    int32_t *actions;      // row r at actions + r * act_stride (6 int32)
+    int64_t act_stride;    // int32 words
+    float *log_prob;       // [rows] (optional)
+    float *value;          // [rows] (optional)
+    int32_t stochastic;    // 0: argmax (best), 1: Gumbel-max sample
+    uint32_t seed, step;   // sample key: threefry({seed, step}, {row, logit})
+};
+
+BB_HD float pol_expf(float x) { return (float)bbm::exp_d((double)x); }
+BB_HD float pol_logf(float x) { return (float)bbm::log_d((double)x); }
+BB_HD float pol_clamp(float x) { return x < -5.f ? -5.f : (x > 5.f ? 5.f : x); }
+BB_HD float pol_relu(float x) { return x > 0.f ? x : 0.f; }
+
+// Gumbel noise of logit i of row r: -log(-log(u)), u in (0, 1).
+BB_HD float pol_gumbel(uint32_t seed, uint32_t step, uint32_t row, uint32_t i)
+{
+    uint32_t b0, b1;
+    threefry2x32(seed, step, row, i, &b0, &b1);
+    const float u = ((float)(b0 >> 8) + 0.5f) * (1.0f / 16777216.0f);
+    return -pol_logf(-pol_logf(u));
+}
+
+// Bucket sampling / scoring of one row's logits.
+BB_HD void pol_select(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
+                      int32_t act[6], float *logp_sum)
+{
+    int o = 0;
+    float total = 0.f;
+    for (int b = 0; b < POL_BUCKETS; b++) {
+        const int nb = pol_bucket(b);
+        float mx = logit[o];
+        for (int i = 1; i < nb; i++) mx = logit[o + i] > mx ? logit[o + i] : mx;
+        int a = 0;
+        if (stochastic) {
+            float best = logit[o] + pol_gumbel(seed, step, row, (uint32_t)o);
+            for (int i = 1; i < nb; i++) {
+                const float g = logit[o + i] + pol_gumbel(seed, step, row, (uint32_t)(o + i));
+                if (g > best) { best = g; a = i; }
+            }
+        } else {
+            for (int i = 1; i < nb; i++)
+                if (logit[o + i] > logit[o + a]) a = i;  // first maximum (torch argmax)
+        }
+        float s = 0.f;
+        for (int i = 0; i < nb; i++) s = s + pol_expf(logit[o + i] - mx);
+        const float lse = mx + pol_logf(s);
+        total = total + (logit[o + a] - lse);
+        act[b] = a;
+        o += nb;
+    }
+    *logp_sum = total;
+}
+
+// Sum of 32 values in the kernel's order: t_c = v_c + v_{c+16}, then the xor
+// butterfly over c in [0, 16) (every lane ends with the same bits).
+BB_HD float pol_sum32(const float *v)
+{
+    float t[16];
+    for (int c = 0; c < 16; c++) t[c] = v[c] + v[c + 16];
+    for (int m = 1; m < 16; m <<= 1) {
+        float u[16];
+        for (int c = 0; c < 16; c++) u[c] = t[c] + t[c ^ m];
+        for (int c = 0; c < 16; c++) t[c] = u[c];
+    }
+    return t[0];
+}
+
+// relu(LayerNorm(h)) in place (torch: biased variance, eps 1e-5).
+BB_HD void pol_layernorm_relu(float *h, const float *w, const float *b)
+{
+    const float mean = pol_sum32(h) * (1.0f / 32.0f);
+    float d[32];
+    for (int c = 0; c < 32; c++) d[c] = h[c] - mean;
+    float sq[32];
+    for (int c = 0; c < 32; c++) sq[c] = d[c] * d[c];
+    const float var = pol_sum32(sq) * (1.0f / 32.0f);
+    const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
+    for (int c = 0; c < 32; c++) h[c] = pol_relu(((d[c] * inv) * w[c]) + b[c]);
+}
+
+// One row on the host, in the kernel's arithmetic order.
+inline void policy_row_host(const PolicyArgs &a, int64_t r)
+{
+    const PolicyWeights &W = a.w;
+    const float *o = a.obs + r * a.obs_stride;
+    float x[POL_IN];
+    for (int k = 0; k < POL_IN; k++) x[k] = pol_clamp((o[k] - W.obs_mean[k]) * W.obs_inv[k]);
+    float h1[POL_HID], h2[POL_HID], out[POL_HEAD];
+    for (int n = 0; n < POL_HID; n++) {
+        float acc = 0.f;
+        for (int j = 0; j < 32; j++)
+            for (int q = 0; q < 4; q++) acc = __builtin_fmaf(x[32 * q + j], W.w1[n * POL_IN + 32 * q + j], acc);
+        h1[n] = acc + W.b1[n];
+    }
+    pol_layernorm_relu(h1, W.ln1_w, W.ln1_b);
+    for (int n = 0; n < POL_HID; n++) {
+        float acc = 0.f;
+        for (int j = 0; j < 8; j++)
+            for (int q = 0; q < 4; q++) acc = __builtin_fmaf(h1[8 * q + j], W.w2[n * POL_HID + 8 * q + j], acc);
+        h2[n] = acc + W.b2[n];
+    }
+    pol_layernorm_relu(h2, W.ln2_w, W.ln2_b);
+    for (int n = 0; n < POL_HEAD; n++) {
+        float acc = 0.f;
+        for (int j = 0; j < 8; j++)
+            for (int q = 0; q < 4; q++) acc = __builtin_fmaf(h2[8 * q + j], W.head_w[n * POL_HID + 8 * q + j], acc);
+        out[n] = acc + W.head_b[n];
+    }
+    int32_t act[6];
+    float lp;
+    pol_select(out, a.stochastic != 0, a.seed, a.step, (uint32_t)r, act, &lp);
+    int32_t *d = a.actions + r * a.act_stride;
+    for (int b = 0; b < 6; b++) d[b] = act[b];
+    if (a.log_prob) a.log_prob[r] = lp;
+    if (a.value) a.value[r] = out[POL_LOGITS];
+}
+
+}  // namespace bb

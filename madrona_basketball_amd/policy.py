@@ -1,0 +1,121 @@
+"""Fused policy inference: the reference's Agent
+(scripts/agent.py:108-154, 32 channels, 2 layers, buckets [2,8,3,2,2,2]) run
+by one gfx950 kernel (bb_policy_forward, csrc/bb_policy.hip) that writes its
+actions straight into the simulator's action tensor -- the
+`actions, log_probs, values = agent(obs)` + `actions[:, i] = a` pair of
+scripts/ppo.py:67 / scripts/env.py:147 without a round trip through torch.
+
+FusedPolicy.from_agent(agent) snapshots the weights of any torch module with
+the reference Agent's layout (obs_norm.mean/var, backbone Linear/LayerNorm,
+actor, critic); call refresh() after an optimizer step.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .madrona import ExecMode
+
+BUCKETS = (2, 8, 3, 2, 2, 2)
+IN, HID, LOGITS, HEAD = 128, 32, 19, 32
+
+
+class FusedPolicy:
+    def __init__(self, device: torch.device):
+        self.device = torch.device(device)
+        self._tensors = {}
+
+    @classmethod
+    def from_agent(cls, agent, device=None) -> "FusedPolicy":
+        dev = device or next(agent.parameters()).device
+        p = cls(dev)
+        p.agent = agent
+        p.refresh()
+        return p
+
+    @torch.no_grad()
+    def refresh(self) -> None:
+        """Re-read the agent's weights (after an update)."""
+        a = self.agent
+        lin = [m for m in a.backbone if isinstance(m, torch.nn.Linear)]
+        lns = [m for m in a.backbone if isinstance(m, torch.nn.LayerNorm)]
+        if (len(lin) != 2 or lin[0].in_features != IN or lin[0].out_features != HID or lin[1].out_features != HID
+                or a.actor.out_features != LOGITS or tuple(a.action_buckets) != BUCKETS):
+            raise ValueError("FusedPolicy supports the reference configuration: input 128, num_channels 32, "
+                             "num_layers 2, buckets [2, 8, 3, 2, 2, 2] (scripts/env.py:107)")
+        dev, f32 = self.device, torch.float32
+
+        def t(x):
+            return x.detach().to(device=dev, dtype=f32).contiguous()
+        # RunningMeanStd.forward (agent.py:29-35): mean/var cast to f32, var + eps, rsqrt
+        mean = a.obs_norm.mean.to(f32)
+        var = a.obs_norm.var.to(f32) + a.obs_norm.epsilon
+        head_w = torch.zeros((HEAD, HID), dtype=f32, device=dev)
+        head_b = torch.zeros((HEAD,), dtype=f32, device=dev)
+        head_w[:LOGITS] = t(a.actor.weight)
+        head_w[LOGITS] = t(a.critic.weight)[0]
+        head_b[:LOGITS] = t(a.actor.bias)
+        head_b[LOGITS] = t(a.critic.bias)[0]
+        self._tensors = {
+            "obs_mean": t(mean), "obs_inv": t(torch.rsqrt(var.to(dev))),
+            "w1": t(lin[0].weight), "b1": t(lin[0].bias), "ln1_w": t(lns[0].weight), "ln1_b": t(lns[0].bias),
+            "w2": t(lin[1].weight), "b2": t(lin[1].bias), "ln2_w": t(lns[1].weight), "ln2_b": t(lns[1].bias),
+            "head_w": head_w, "head_b": head_b,
+        }
+        self._w = _lib.PolicyWeights(**{k: v.data_ptr() for k, v in self._tensors.items()})
+
+    def to(self, device) -> "FusedPolicy":
+        """A copy of the packed weights on another device (same bits)."""
+        p = FusedPolicy(device)
+        p.agent = getattr(self, "agent", None)
+        p._tensors = {k: v.to(p.device).contiguous() for k, v in self._tensors.items()}
+        p._w = _lib.PolicyWeights(**{k: v.data_ptr() for k, v in p._tensors.items()})
+        return p
+
+    def _stream(self):
+        if self.device.type == "cuda":
+            return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        return ctypes.c_void_p(None)
+
+    def forward_into(self, obs: torch.Tensor, actions: torch.Tensor, log_prob: torch.Tensor = None,
+                     value: torch.Tensor = None, stochastic: bool = True, seed: int = 0, step: int = 0) -> None:
+        """obs [R, >=128] float32 rows (any row stride, e.g. obs_tensor[:, agent]);
+        actions [R, 6] int32 rows (any row stride, e.g. action_tensor[:, agent])."""
+        rows = obs.shape[0]
+        if obs.dim() != 2 or obs.shape[1] < IN or obs.stride(1) != 1 or obs.dtype != torch.float32:
+            raise ValueError("obs must be float32 [rows, >=128] with unit column stride")
+        if (actions.dim() != 2 or actions.shape != (rows, 6) or actions.stride(1) != 1
+                or actions.dtype != torch.int32):
+            raise ValueError("actions must be int32 [rows, 6] with unit column stride")
+        for t in (obs, actions, log_prob, value):
+            if t is not None and t.device != self.device:
+                raise ValueError("all tensors must live on the policy's device")
+        for t in (log_prob, value):
+            if t is not None and (t.shape != (rows,) or not t.is_contiguous() or t.dtype != torch.float32):
+                raise ValueError("log_prob / value must be contiguous float32 [rows]")
+        mode = ExecMode.CUDA if self.device.type == "cuda" else ExecMode.CPU
+        _lib.check(_lib.load().bb_policy_forward(
+            ctypes.byref(self._w), int(mode), self.device.index if self.device.index is not None else -1,
+            ctypes.c_void_p(obs.data_ptr()), rows, obs.stride(0), ctypes.c_void_p(actions.data_ptr()),
+            actions.stride(0), ctypes.c_void_p(None if log_prob is None else log_prob.data_ptr()),
+            ctypes.c_void_p(None if value is None else value.data_ptr()), 1 if stochastic else 0,
+            int(seed) & 0xFFFFFFFF, int(step) & 0xFFFFFFFF, self._stream()), "policy_forward")
+
+    def __call__(self, obs: torch.Tensor, stochastic: bool = True, seed: int = 0, step: int = 0):
+        """Agent.forward's outputs (actions int32 [R, 6], log_probs [R], values [R])."""
+        rows = obs.shape[0]
+        actions = torch.empty((rows, 6), dtype=torch.int32, device=self.device)
+        lp = torch.empty((rows,), dtype=torch.float32, device=self.device)
+        v = torch.empty((rows,), dtype=torch.float32, device=self.device)
+        self.forward_into(obs, actions, lp, v, stochastic, seed, step)
+        return actions, lp, v
+
+    def act(self, sim, agent_idx: int, log_prob: torch.Tensor = None, value: torch.Tensor = None,
+            stochastic: bool = True, seed: int = 0, step: int = 0) -> None:
+        """Observe agent `agent_idx` of every world and write its actions into the
+        simulator's action tensor (env.py:147's `actions[:, i] = a`), on the device."""
+        obs = sim.observations_tensor().to_torch()[:, agent_idx]
+        act = sim.action_tensor().to_torch()[:, agent_idx]
+        self.forward_into(obs, act, log_prob, value, stochastic, seed, step)
