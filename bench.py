@@ -91,6 +91,9 @@ def main():
     ap.add_argument("--rollout", type=int, default=0,
                     help="K > 0: bb_rollout of K steps per call (observations / rewards / dones recorded "
                          "into [K, W, N, ...] buffers; one k_rollout launch at 2 agents); 0: one step per call")
+    ap.add_argument("--policy", action="store_true",
+                    help="every step: the fused policy (reference Agent, random init) acts for every agent "
+                         "into the action tensor, then the step (env.py + ppo.py's inference, on the device)")
     ap.add_argument("--no-record", action="store_true",
                     help="diagnostics: rollouts without recorded outputs (each step rewrites the sim's own tensors)")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
@@ -158,8 +161,20 @@ def main():
             raise SystemExit("--steps must be a multiple of --rollout")
         bufs = sim.rollout_buffers(K)  # reused by every chunk, like PPO's storage between updates
 
+    if args.policy:
+        from madrona_basketball_amd.policy import FusedPolicy, make_agent
+        pol = FusedPolicy.from_agent(make_agent(0).to(dev))
+        lp = torch.empty((W,), dtype=torch.float32, device=dev)
+        val = torch.empty((W,), dtype=torch.float32, device=dev)
+
     def run(actions, time_kernels=False):
         """All staged steps: one step per launch, or chunks of K via bb_rollout."""
+        if args.policy:  # actions come from the policy, not the staged rows
+            for t in range(args.steps):
+                for a in range(args.agents):
+                    pol.act(sim, a, lp, val, stochastic=True, seed=args.seed, step=t)
+                sim.step()
+            return None
         if not K:
             return sim.step_n_staged(actions, time_kernels=time_kernels)
         ms = 0.0
@@ -183,7 +198,7 @@ def main():
     # kernel timing: the step kernel's own start/end (hipExtLaunchKernel
     # events on the launch stream) over the same workload, re-staged
     launches = args.steps // K if (K and fused) else args.steps
-    if on_gpu:
+    if on_gpu and not args.policy:
         staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup + args.steps)
         barrier()
         kernel_ms = run(staged, time_kernels=True)
@@ -225,7 +240,9 @@ def main():
                         f"NUM_AGENTS={args.agents}), threefry random actions per step (buckets "
                         f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
                         + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
-                           f"of every step recorded into [{K}, W, N, ...] buffers" if K else "; one step per call"),
+                           f"of every step recorded into [{K}, W, N, ...] buffers" if K else "; one step per call")
+                        + ("; actions from the fused policy (reference Agent layout, random init, Gumbel "
+                           "sampling) for every agent before each step" if args.policy else ""),
             "worlds_per_gpu": W,
             "total_worlds": total_worlds,
             "agents_per_world": args.agents,
@@ -246,6 +263,8 @@ def main():
     if not on_gpu:
         out["roofline"] = None
         out["config"]["parallelism"] += " (host executor, gloo)"
+    if args.policy:
+        out["roofline"] = None  # several kernels per step: see the rocprof summary
     if rank == 0:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -13,7 +13,7 @@
 // fmaf chain the gfx950 f32 MFMA computes (v_mfma_f32_16x16x4_f32: one rounding per
 // product), over the k permutation the kernel's operand layout gives -- k = 32q + j for
 // the 128-wide layer (j outer, q inner), k = 8q + j for the 32-wide ones; LayerNorm
-// sums are the kernel's butterfly tree.  exp / log: bb_math (correctly rounded floats).
+// sums are the kernel's butterfly tree (DPP), exp / log fixed f32 sequences (below).
 #pragma once
 #include "bb_math.h"
 #include "bb_rng.h"
@@ -48,45 +48,95 @@ struct PolicyArgs {
     uint32_t seed, step;   // sample key: threefry({seed, step}, {row, logit})
 };
 
-BB_HD float pol_expf(float x) { return (float)bbm::exp_d((double)x); }
-BB_HD float pol_logf(float x) { return (float)bbm::log_d((double)x); }
-BB_HD float pol_clamp(float x) { return x < -5.f ? -5.f : (x > 5.f ? 5.f : x); }
+// exp / log in f32 from a fixed sequence of f32 operations (identical bits on
+// host and gfx950; ~1 ulp): the policy is compared with torch's fp32 forward
+// within a tolerance, so the step's correctly-rounded double route (bb_math)
+// is not needed here, and these are 4-8x cheaper.
+BB_HD float pol_expf(float x)
+{
+    if (x != x) return x;
+    if (x > 88.7f) return __builtin_inff();
+    if (x < -103.9f) return 0.f;
+    const float k = __builtin_rintf(x * 1.44269504f);
+    float r = x - k * 0.693145752f;          // ln2 high part (exact product for |k| < 2^11)
+    r = r - k * 1.42860677e-06f;             // ln2 low part
+    float p = 1.0f / 5040.0f;                // Taylor to r^7 on |r| <= 0.347
+    p = p * r + 1.0f / 720.0f;
+    p = p * r + 1.0f / 120.0f;
+    p = p * r + 1.0f / 24.0f;
+    p = p * r + 1.0f / 6.0f;
+    p = p * r + 0.5f;
+    p = p * r + 1.0f;
+    p = p * r + 1.0f;
+    return __builtin_ldexpf(p, (int)k);
+}
+BB_HD float pol_logf(float x)
+{
+    if (x != x || x < 0.f) return __builtin_nanf("");
+    if (x == 0.f) return -__builtin_inff();
+    if (x == __builtin_inff()) return x;
+    int e = 0;
+    float m = __builtin_frexpf(x, &e);       // [0.5, 1)
+    if (m < 0.707106781f) { m = m * 2.0f; e -= 1; }
+    const float s = (m - 1.0f) / (m + 1.0f);  // |s| <= 0.1716
+    const float z = s * s;
+    float p = 1.0f / 11.0f;
+    p = p * z + 1.0f / 9.0f;
+    p = p * z + 1.0f / 7.0f;
+    p = p * z + 1.0f / 5.0f;
+    p = p * z + 1.0f / 3.0f;
+    const float lm = 2.0f * (s + (s * z) * p);
+    const float k = (float)e;
+    return k * 0.693145752f + (k * 1.42860677e-06f + lm);
+}
+BB_HD float pol_clamp(float x) { return __builtin_fminf(__builtin_fmaxf(x, -5.f), 5.f); }  // v_max / v_min
 BB_HD float pol_relu(float x) { return x > 0.f ? x : 0.f; }
 
-// Gumbel noise of logit i of row r: -log(-log(u)), u in (0, 1).
+// Gumbel noise of logit i of row r: -log(-log(u)), u in (0, 1); one threefry
+// call serves logits 2p and 2p + 1 (its two output words).
+BB_HD float pol_u01_open(uint32_t bits) { return ((float)(bits >> 8) + 0.5f) * (1.0f / 16777216.0f); }
 BB_HD float pol_gumbel(uint32_t seed, uint32_t step, uint32_t row, uint32_t i)
 {
     uint32_t b0, b1;
-    threefry2x32(seed, step, row, i, &b0, &b1);
-    const float u = ((float)(b0 >> 8) + 0.5f) * (1.0f / 16777216.0f);
-    return -pol_logf(-pol_logf(u));
+    threefry2x32(seed, step, row, i >> 1, &b0, &b1);
+    return -pol_logf(-pol_logf(pol_u01_open((i & 1u) ? b1 : b0)));
 }
 
-// Bucket sampling / scoring of one row's logits.
+// Bucket sampling / scoring of one row's logits (fully unrolled: the bucket
+// sizes and offsets are compile-time, so logit[] stays in registers).
 BB_HD void pol_select(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
                       int32_t act[6], float *logp_sum)
 {
     int o = 0;
     float total = 0.f;
+#pragma unroll
     for (int b = 0; b < POL_BUCKETS; b++) {
         const int nb = pol_bucket(b);
         float mx = logit[o];
+#pragma unroll
         for (int i = 1; i < nb; i++) mx = logit[o + i] > mx ? logit[o + i] : mx;
         int a = 0;
         if (stochastic) {
             float best = logit[o] + pol_gumbel(seed, step, row, (uint32_t)o);
+#pragma unroll
             for (int i = 1; i < nb; i++) {
                 const float g = logit[o + i] + pol_gumbel(seed, step, row, (uint32_t)(o + i));
                 if (g > best) { best = g; a = i; }
             }
         } else {
+            float best = logit[o];
+#pragma unroll
             for (int i = 1; i < nb; i++)
-                if (logit[o + i] > logit[o + a]) a = i;  // first maximum (torch argmax)
+                if (logit[o + i] > best) { best = logit[o + i]; a = i; }  // first maximum (torch argmax)
         }
         float s = 0.f;
+#pragma unroll
         for (int i = 0; i < nb; i++) s = s + pol_expf(logit[o + i] - mx);
         const float lse = mx + pol_logf(s);
-        total = total + (logit[o + a] - lse);
+        float la = logit[o];
+#pragma unroll
+        for (int i = 1; i < nb; i++) la = a == i ? logit[o + i] : la;
+        total = total + (la - lse);
         act[b] = a;
         o += nb;
     }

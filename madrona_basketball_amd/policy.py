@@ -22,6 +22,39 @@ BUCKETS = (2, 8, 3, 2, 2, 2)
 IN, HID, LOGITS, HEAD = 128, 32, 19, 32
 
 
+class _ObsNorm(torch.nn.Module):
+    """RunningMeanStd's state (scripts/agent.py:19-26): float64 mean / var, eps."""
+
+    def __init__(self, dim: int):
+        super().__init__()
+        self.epsilon = 1e-5
+        self.register_buffer("mean", torch.zeros(dim, dtype=torch.float64))
+        self.register_buffer("var", torch.ones(dim, dtype=torch.float64))
+
+
+def make_agent(seed: int = 0) -> torch.nn.Module:
+    """A torch module with the reference Agent's layout and initialisation
+    (scripts/agent.py:97-131: Kaiming-normal backbone, orthogonal heads at gain
+    0.01, zero biases, identity observation normaliser) -- random weights of
+    that architecture for benchmarks and tests (no checkpoints here)."""
+    g = torch.Generator().manual_seed(seed)
+    m = torch.nn.Module()
+    m.action_buckets = list(BUCKETS)
+    m.backbone = torch.nn.Sequential(torch.nn.Linear(IN, HID), torch.nn.LayerNorm(HID), torch.nn.ReLU(),
+                                     torch.nn.Linear(HID, HID), torch.nn.LayerNorm(HID), torch.nn.ReLU())
+    m.actor = torch.nn.Linear(HID, LOGITS)
+    m.critic = torch.nn.Linear(HID, 1)
+    m.obs_norm = _ObsNorm(IN)
+    with torch.no_grad():
+        for lin in (m.backbone[0], m.backbone[3]):
+            torch.nn.init.kaiming_normal_(lin.weight, torch.nn.init.calculate_gain("relu"), generator=g)
+            lin.bias.zero_()
+        for lin in (m.actor, m.critic):
+            torch.nn.init.orthogonal_(lin.weight, gain=0.01, generator=g)
+            lin.bias.zero_()
+    return m
+
+
 class FusedPolicy:
     def __init__(self, device: torch.device):
         self.device = torch.device(device)

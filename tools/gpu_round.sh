@@ -52,6 +52,11 @@ for s in $STEPS; do
         python3 tools/traffic.py "$OUT/pmcr${k}_fetch" "$OUT/pmcr${k}_write" W65536_N2_R$k --kernel "k_rollout<2>" \
             --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
         ;;
+    benchp) run bench_policy 600 python bench.py --steps 300 --warmup 30 --policy --no-cpu-baseline ;;
+    profp)
+        ( cd /tmp && export TMPDIR=/tmp && run prof_policy 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_policy" -o run \
+            --output-format csv -- python3 "$ROOT/bench.py" --steps 200 --warmup 20 --policy --no-cpu-baseline ) || exit $?
+        ;;
     rtests) run pytest_rollout 600 python -u -m pytest tests/test_rollout.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     benchr:*) k=${s#benchr:}; run "bench_r$k" 600 python bench.py --steps 1024 --warmup 64 --rollout $k --no-cpu-baseline ;;
     profr:*) k=${s#profr:}

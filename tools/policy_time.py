@@ -1,0 +1,51 @@
+"""Average k_policy time (torch events on the current stream) for argmax and
+sampling, over a simulator's real observation rows.
+
+python tools/policy_time.py [--worlds 65536] [--iters 50]
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--worlds", type=int, default=65536)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--only-argmax", action="store_true", help="agent-0 rows, argmax only (PMC runs)")
+    a = ap.parse_args()
+    import madrona_basketball_amd as mba
+    from madrona_basketball_amd.policy import FusedPolicy, make_agent
+    sim = mba.SimpleGridworldSimulator(32, 17, 15.7575, 8.382, 39600, mba.ExecMode.CUDA, a.worlds, 0,
+                                       per_world_rng=True)
+    sim.step_n(100, random_actions=True)
+    pol = FusedPolicy.from_agent(make_agent(0).cuda())
+    obs_all = sim.observations_tensor().to_torch()
+    cases = [("agent 0 rows", obs_all[:, 0])]
+    if not a.only_argmax:
+        cases.append(("all agents", obs_all.view(-1, obs_all.shape[-1])))
+    for label, obs in cases:
+        rows = obs.shape[0]
+        act = torch.empty((rows, 6), dtype=torch.int32, device="cuda")
+        lp = torch.empty(rows, device="cuda")
+        v = torch.empty(rows, device="cuda")
+        for stoch in ((False,) if a.only_argmax else (False, True)):
+            pol.forward_into(obs, act, lp, v, stochastic=stoch)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for t in range(a.iters):
+                pol.forward_into(obs, act, lp, v, stochastic=stoch, step=t)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / a.iters
+            print(f"{label:14s} rows {rows:7d} stochastic={int(stoch)}  {us:8.2f} us/launch  "
+                  f"{rows * 512 / us / 1e3:7.1f} GB/s of obs rows", flush=True)
+
+
+if __name__ == "__main__":
+    main()
