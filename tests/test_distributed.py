@@ -77,3 +77,49 @@ def test_sharded_ranks_equal_single_process():
     full = make_sim(ExecMode.CPU, W, per_world_rng=True)
     full.step_n(steps, random_actions=True, action_seed=5)
     assert np.array_equal(got.view(np.uint32), full.observations_tensor().to_torch().numpy().view(np.uint32))
+
+
+def _rollout_worker(rank, world, port, W, K, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    shard = W // world
+    sim = make_sim(ExecMode.CPU, shard, per_world_rng=True, world_offset=rank * shard)
+    acts = sim.stage_random_actions(K, action_seed=8, step0=0)  # keyed by global world index
+    buf = sim.rollout_buffers(K)
+    sim.rollout(acts, buf["obs"], buf["reward"], buf["done"])
+    out = []
+    for key in ("obs", "reward", "done"):
+        t = buf[key].transpose(0, 1).contiguous()  # worlds first for the gather
+        g = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(g, t)
+        out.append(torch.cat(g).transpose(0, 1).contiguous())
+    if rank == 0:
+        q.put([o.numpy() for o in out])
+    dist.destroy_process_group()
+
+
+def test_sharded_rollouts_equal_single_process():
+    """World-sharded K-step rollouts (bb_rollout, no collective on the path)
+    gather to the unsharded rollout's recorded outputs, bit for bit."""
+    W, K = 96, 40
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_rollout_worker, args=(r, 2, port, W, K, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    full = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    acts = full.stage_random_actions(K, action_seed=8, step0=0)
+    buf = full.rollout_buffers(K)
+    full.rollout(acts, buf["obs"], buf["reward"], buf["done"])
+    for g, key in zip(got, ("obs", "reward", "done")):
+        assert np.array_equal(g.view(np.uint32), buf[key].numpy().view(np.uint32)), key

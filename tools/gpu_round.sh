@@ -41,7 +41,7 @@ run() {  # name timeout cmd...
 for s in $STEPS; do
     case $s in
     smoke) run smoke 420 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rA ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread ;;
     bench) run bench 600 python bench.py --steps 1000 --warmup 100 ;;
     rectests) run pytest_recorder 600 python -u -m pytest tests/test_recorder.py -m gpu -x -v --timeout 300 --timeout-method thread ;;
     pmcr:*) k=${s#pmcr:}
