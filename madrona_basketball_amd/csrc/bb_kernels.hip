@@ -556,7 +556,13 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
 // world-level systems on it together (same instructions, same values); the
 // per-agent systems are computed by the agent's lane and exchanged through
 // an LDS buffer (LdsAgents).  No per-lane copy of the world: nothing to spill.
-constexpr int XW = 32;  // words per lane in the exchange buffer (>= Intrinsic)
+#ifndef BB_XW
+#define BB_XW 33
+#endif
+// Words per lane in the exchange buffer (>= Intrinsic).  Odd, so that the
+// rows lanes of different worlds read at once fall in different LDS banks
+// (at 32 words the row start is 0 or 32 mod 64 banks: up to 30-way conflicts).
+constexpr int XW = BB_XW;
 
 template <int N, int MODE>
 struct LdsAgents {
