@@ -3,19 +3,21 @@
 //
 // The reference calls libm: sinf/cosf/atan2f/atanf/acosf on floats and the
 // double overloads of erf/acos/exp (src/game.cpp:302,345,435,746,806,808,868;
-// src/helper.cpp:39,135-136).  Its two executors disagree with each other in
-// the last ulp (glibc on the CPU executor, CUDA libdevice under NVRTC), so this
-// build fixes one platform-independent definition:
+// src/helper.cpp:39,135-136).  Its CPU TaskGraph executor -- the north_star's
+// parity target -- gets them from glibc.  So:
 //
-//     float  f(float x)   :=  (float) f_binary64(x)
+//   * the float functions are glibc 2.35's own algorithms, restated operation
+//     for operation (section "float API" below; exhaustively equal to the
+//     host libm on every float input, tests/test_math.py);
+//   * the double functions (erf, exp, acos on a float argument, rounded back
+//     to float by the reference) are evaluated here from IEEE-754 binary64
+//     add/mul/fma/div/sqrt only (Horner / Taylor kernels, tables from
+//     tools/gen_math_tables.py), within ~1 double ulp of libm's: their float
+//     results equal libm's except within ~2^-29 relative of a float rounding
+//     boundary (tests/test_math.py).
 //
-// where f_binary64 is evaluated here from IEEE-754 binary64 add/mul/fma/div/
-// sqrt only (Cody-Waite reduction + Taylor/Horner kernels, tables from
-// tools/gen_math_tables.py).  Every f_binary64 is within ~1 ulp of the true
-// value, so the float result is the correctly rounded one except for inputs
-// within ~2^-28 relative of a float rounding boundary (tested against
-// (float)libm_double(x) in tests/test_math.py).  Compile with
-// -ffp-contract=off: every product and sum below is meant to round on its own.
+// Compile with -ffp-contract=off: every product and sum below is meant to
+// round on its own; fused multiply-adds are written as fma_d.
 #pragma once
 #include <stdint.h>
 
@@ -52,85 +54,12 @@ static constexpr double PI_LO = 1.2246467991473532e-16;
 static constexpr double PIO2_HI = 1.5707963267948966;
 static constexpr double PIO2_LO = 6.123233995736766e-17;
 
-// pi/2 split in 33-bit pieces (Cody-Waite), 2/pi, ln2 split (32-bit high part).
-static constexpr double INV_PIO2 = 6.36619772367581382433e-01;
-static constexpr double PIO2_1 = 1.57079632673412561417e+00;
-static constexpr double PIO2_2 = 6.07710050630396597660e-11;
-static constexpr double PIO2_3 = 2.02226624871116645580e-21;
+// ln2 split (32-bit high part).
 static constexpr double INV_LN2 = 1.44269504088896338700e+00;
 static constexpr double LN2_HI = 6.93147180369123816490e-01;
 static constexpr double LN2_LO = 1.90821492927058770002e-10;
 static constexpr double TWO_OVER_SQRTPI = 1.1283791670955126;   // 2/sqrt(pi)
 static constexpr double INV_SQRTPI = 0.5641895835477563;        // 1/sqrt(pi)
-
-// ---------------------------------------------------------------- sin / cos
-// Kernels on |r| <= pi/4 (+ rounding slack): Taylor to r^23 / r^22.
-BB_HD double sin_kernel(double r)
-{
-    const double z = r * r;
-    double p = -1.0 / 25852016738884976640000.0;   // -1/23!
-    p = fma_d(p, z, 1.0 / 51090942171709440000.0);  // 1/21!
-    p = fma_d(p, z, -1.0 / 121645100408832000.0);   // -1/19!
-    p = fma_d(p, z, 1.0 / 355687428096000.0);       // 1/17!
-    p = fma_d(p, z, -1.0 / 1307674368000.0);        // -1/15!
-    p = fma_d(p, z, 1.0 / 6227020800.0);            // 1/13!
-    p = fma_d(p, z, -1.0 / 39916800.0);             // -1/11!
-    p = fma_d(p, z, 1.0 / 362880.0);                // 1/9!
-    p = fma_d(p, z, -1.0 / 5040.0);                 // -1/7!
-    p = fma_d(p, z, 1.0 / 120.0);                   // 1/5!
-    p = fma_d(p, z, -1.0 / 6.0);                    // -1/3!
-    return fma_d(r * z, p, r);
-}
-
-BB_HD double cos_kernel(double r)
-{
-    const double z = r * r;
-    double q = -1.0 / 1124000727777607680000.0;     // -1/22!
-    q = fma_d(q, z, 1.0 / 2432902008176640000.0);   // 1/20!
-    q = fma_d(q, z, -1.0 / 6402373705728000.0);     // -1/18!
-    q = fma_d(q, z, 1.0 / 20922789888000.0);        // 1/16!
-    q = fma_d(q, z, -1.0 / 87178291200.0);          // -1/14!
-    q = fma_d(q, z, 1.0 / 479001600.0);             // 1/12!
-    q = fma_d(q, z, -1.0 / 3628800.0);              // -1/10!
-    q = fma_d(q, z, 1.0 / 40320.0);                 // 1/8!
-    q = fma_d(q, z, -1.0 / 720.0);                  // -1/6!
-    q = fma_d(q, z, 1.0 / 24.0);                    // 1/4!
-    // cos r = 1 - z/2 + z^2 q, with the 1 - z/2 split kept exact (fdlibm style)
-    const double hz = 0.5 * z;
-    const double w = 1.0 - hz;
-    return w + fma_d(z * z, q, (1.0 - w) - hz);
-}
-
-// x -> (r, quadrant) with x = r + k pi/2; exact-enough for |x| < 2^20 pi/2.
-BB_HD double reduce_pio2(double x, int *quadrant)
-{
-    const double k = rint_d(x * INV_PIO2);
-    double r = fma_d(-k, PIO2_1, x);
-    r = fma_d(-k, PIO2_2, r);
-    r = fma_d(-k, PIO2_3, r);
-    *quadrant = (int)((int64_t)k & 3);
-    return r;
-}
-
-BB_HD void sincos_d(double x, double *s, double *c)
-{
-    if (!(fabs_d(x) <= 1.0e15)) {   // NaN, inf, absurd angles: deterministic junk
-        *s = x - x; *c = x - x;
-        return;
-    }
-    int q;
-    const double r = reduce_pio2(x, &q);
-    const double sr = sin_kernel(r), cr = cos_kernel(r);
-    switch (q) {
-    case 0: *s = sr; *c = cr; break;
-    case 1: *s = cr; *c = -sr; break;
-    case 2: *s = -sr; *c = -cr; break;
-    default: *s = -cr; *c = sr; break;
-    }
-}
-
-BB_HD double sin_d(double x) { double s, c; sincos_d(x, &s, &c); return s; }
-BB_HD double cos_d(double x) { double s, c; sincos_d(x, &s, &c); return c; }
 
 // ---------------------------------------------------------------- atan family
 // atan on [0, 1]: atan(t) = atan(c) + atan((t - c) / (1 + t c)), c = i/8.
@@ -324,18 +253,254 @@ BB_HD double erf_d(double x, const double *tab = &ERF_TAYLOR[0][0])
     return signbit_d(x) ? -r : r;
 }
 
-// ---------------------------------------------------------------- float API
-BB_HD float sinf_(float x) { return (float)sin_d((double)x); }
-BB_HD float cosf_(float x) { return (float)cos_d((double)x); }
+// ------------------------------------------------ float API: glibc 2.35 libm
+// The reference CPU executor calls glibc's float functions (sinf/cosf/atan2f/
+// atanf/acosf; src/game.cpp:302,345,435,806, src/helper.cpp:39,135-136).
+// What follows restates glibc 2.35's x86-64 implementations operation for
+// operation, so the step computes exactly what the reference CPU executor
+// computes on the same inputs:
+//   * sinf / cosf: the double-precision polynomial implementation
+//     (sysdeps/ieee754/flt-32/s_sinf.c, s_cosf.c, sincosf.h) in its FMA ifunc
+//     variant (selected on every AVX2+FMA host): the fused multiply-adds below
+//     are exactly those of that variant; coefficient table __sincosf_table;
+//   * atanf, atan2f, acosf: the single-precision fdlibm implementations
+//     (s_atanf.c, e_atan2f.c, e_acosf.c; no ifunc variants), every float
+//     operation rounding on its own (-ffp-contract=off).
+// Constants are the words the library holds.  Pinned exhaustively (every
+// float input) against the host's libm by tests/test_math.py.
+BB_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+BB_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+BB_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
+
+// __sincosf_table[0]: 2/pi 2^24, pi/2 and the polynomial coefficients.
+// __sincosf_table[1] (quadrants 2-3) holds the cosine coefficients negated:
+// every fused step of the cosine polynomial then yields the exact negation,
+// so it is applied as one sign flip of the result (no per-lane table reads).
+static constexpr double GLIBC_HPI_INV = 10680707.430881744, GLIBC_HPI = 1.5707963267948966;
+static constexpr double GLIBC_C0 = 1.0, GLIBC_C1 = -0.49999999725108224, GLIBC_C2 = 0.041666623324344516,
+                        GLIBC_C3 = -0.001388676379437604, GLIBC_C4 = 2.4390450703564542e-05;
+static constexpr double GLIBC_S1 = -0.16666654943701084, GLIBC_S2 = 0.008332178146138854,
+                        GLIBC_S3 = -0.00019517298981385725;
+// __inv_pio4: 4/pi in 32-bit words, for the |x| >= 120 reduction
+static constexpr uint32_t GLIBC_INV_PIO4[24] = {
+    0xa2, 0xa2f9, 0xa2f983, 0xa2f9836e, 0xf9836e4e, 0x836e4e44, 0x6e4e4415, 0x4e441529,
+    0x441529fc, 0x1529fc27, 0x29fc2757, 0xfc2757d1, 0x2757d1f5, 0x57d1f534, 0xd1f534dd, 0xf534ddc0,
+    0x34ddc0db, 0xddc0db62, 0xc0db6295, 0xdb629599, 0x6295993c, 0x95993c43, 0x993c4390, 0x3c439041,
+};
+
+// sinf_poly's two branches (sincosf.h)
+BB_HD float glibc_sin_poly(double x, double x2)
+{
+    const double x3 = x2 * x;
+    const double s1 = fma_d(x2, GLIBC_S3, GLIBC_S2);
+    const double x5 = x2 * x3;
+    const double s = fma_d(x3, GLIBC_S1, x);
+    return (float)fma_d(s1, x5, s);
+}
+BB_HD float glibc_cos_poly(double x2)
+{
+    const double x4 = x2 * x2;
+    const double c1 = fma_d(x2, GLIBC_C1, GLIBC_C0);
+    const double c2 = fma_d(x2, GLIBC_C4, GLIBC_C3);
+    const double x6 = x2 * x4;
+    const double c = fma_d(x4, GLIBC_C2, c1);
+    return (float)fma_d(c2, x6, c);
+}
+// x = n pi/2 + r for |x| < 120: n = round(x 2/pi) from the 2^24-scaled
+// product, r by one fused multiply-add (reduce_fast).
+BB_HD double glibc_reduce_fast(double x, int *np)
+{
+    const double r = x * GLIBC_HPI_INV;
+    const int n = ((int32_t)r + 0x800000) >> 24;
+    *np = n;
+    return fma_d(-(double)n, GLIBC_HPI, x);
+}
+// |x| >= 120: 4/pi in fixed point times the significand (reduce_large).
+BB_HD double glibc_reduce_large(uint32_t xi, int *np)
+{
+    const uint32_t *arr = &GLIBC_INV_PIO4[(xi >> 26) & 15];
+    const int shift = (xi >> 23) & 7;
+    xi = (xi & 0xffffff) | 0x800000;
+    xi <<= shift;
+    uint64_t res0 = (uint64_t)(uint32_t)(xi * arr[0]);
+    const uint64_t res1 = (uint64_t)xi * arr[4];
+    const uint64_t res2 = (uint64_t)xi * arr[8];
+    res0 = (res2 >> 32) | (res0 << 32);
+    res0 += res1;
+    const uint64_t n = (res0 + (1ull << 61)) >> 62;
+    res0 -= n << 62;
+    *np = (int)n;
+    return (double)(int64_t)res0 * u2d(0x3c1921fb54442d18ull);  // pi / 2^63
+}
+// sinf (cos = false) or cosf (cos = true)
+BB_HD float glibc_sincosf_one(float y, bool cos)
+{
+    const uint32_t top = (f2u(y) >> 20) & 0x7ff;
+    double x = (double)y;
+    if (top < 0x3f4) {  // |y| < pi/4
+        const double x2 = x * x;
+        if (top < 0x398) return cos ? 1.0f : y;  // |y| < 2^-12
+        return cos ? glibc_cos_poly(x2) : glibc_sin_poly(x, x2);
+    }
+    int n, q;  // q selects the sign and the table: n, plus the sign of y on the large path
+    if (top < 0x42f) {  // |y| < 120
+        x = glibc_reduce_fast(x, &n);
+        q = n;
+    } else if (top < 0x7f8) {
+        x = glibc_reduce_large(f2u(y), &n);
+        q = n + (int)(f2u(y) >> 31);
+    } else {
+        return (y - y) / (y - y);  // inf / nan: invalid
+    }
+    const double x2 = x * x;
+    if (((n & 1) != 0) != cos) {
+        const float c = glibc_cos_poly(x2);
+        return (q & 2) ? -c : c;
+    }
+    return glibc_sin_poly(((q + 1) & 2) ? -x : x, x2);  // sign[q & 3] = {1, -1, -1, 1}
+}
+
+// fdlibm s_atanf.c as glibc builds it
+BB_HD float glibc_atanf(float x)
+{
+    const uint32_t hx = f2u(x), ix = hx & 0x7fffffff;
+    const float aT[11] = {u2f(0x3eaaaaab), u2f(0xbe4ccccd), u2f(0x3e124925), u2f(0xbde38e38), u2f(0x3dba2e6e),
+                          u2f(0xbd9d8795), u2f(0x3d886b35), u2f(0xbd6ef16b), u2f(0x3d4bda59), u2f(0xbd15a221),
+                          u2f(0x3c8569d7)};
+    // atanhi / atanlo[id] by selects (no per-lane table)
+    const auto hi = [](int id) {
+        return u2f(id == 0 ? 0x3eed6338u : id == 1 ? 0x3f490fdau : id == 2 ? 0x3f7b985eu : 0x3fc90fdau);
+    };
+    const auto lo = [](int id) {
+        return u2f(id == 0 ? 0x31ac3769u : id == 1 ? 0x33222168u : id == 2 ? 0x33140fb4u : 0x33a22168u);
+    };
+    if (ix >= 0x4c000000) {  // |x| >= 2^25
+        if (ix > 0x7f800000) return x + x;
+        return (int32_t)hx > 0 ? lo(3) + hi(3) : -hi(3) - lo(3);
+    }
+    int id;
+    if (ix < 0x3ee00000) {  // |x| < 0.4375
+        if (ix < 0x31000000) return x;  // |x| < 2^-29 (huge + x > one)
+        id = -1;
+    } else {
+        x = __builtin_fabsf(x);
+        if (ix < 0x3f980000) {      // |x| < 1.1875
+            if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
+                id = 0; x = ((x + x) - 1.0f) / (x + 2.0f);
+            } else {                // 11/16 <= |x| < 19/16
+                id = 1; x = (x - 1.0f) / (x + 1.0f);
+            }
+        } else if (ix < 0x401c0000) {  // |x| < 2.4375
+            id = 2; x = (x - 1.5f) / (x * 1.5f + 1.0f);
+        } else {                       // 2.4375 <= |x| < 2^25
+            id = 3; x = -1.0f / x;
+        }
+    }
+    const float z = x * x;
+    const float w = z * z;
+    const float s1 = z * (aT[0] + w * (aT[2] + w * (aT[4] + w * (aT[6] + w * (aT[8] + w * aT[10])))));
+    const float s2 = w * (aT[1] + w * (aT[3] + w * (aT[5] + w * (aT[7] + w * aT[9]))));
+    if (id < 0) return x - x * (s1 + s2);
+    const float r = hi(id) - ((x * (s1 + s2) - lo(id)) - x);
+    return (int32_t)hx < 0 ? -r : r;
+}
+
+// fdlibm e_atan2f.c as glibc builds it (__ieee754_atan2f; the wrapper only
+// sets errno)
+BB_HD float glibc_atan2f(float y, float x)
+{
+    const float tiny = u2f(0x0da24260), pi_o_4 = u2f(0x3f490fdb), pi_o_2 = u2f(0x3fc90fdb),
+                pi = u2f(0x40490fdb), pi_lo = u2f(0xb3bbbd2e);
+    const uint32_t hx = f2u(x), ix = hx & 0x7fffffff, hy = f2u(y), iy = hy & 0x7fffffff;
+    if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+    if (hx == 0x3f800000) return glibc_atanf(y);
+    const int m = (int)((hy >> 31) & 1) | (int)((hx >> 30) & 2);
+    if (iy == 0) {
+        switch (m) {
+        case 0: case 1: return y;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (ix == 0) return (int32_t)hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    if (ix == 0x7f800000) {
+        if (iy == 0x7f800000) {
+            switch (m) {
+            case 0: return pi_o_4 + tiny;
+            case 1: return -pi_o_4 - tiny;
+            case 2: return 3.0f * pi_o_4 + tiny;
+            default: return -3.0f * pi_o_4 - tiny;
+            }
+        }
+        switch (m) {
+        case 0: return 0.0f;
+        case 1: return -0.0f;
+        case 2: return pi + tiny;
+        default: return -pi - tiny;
+        }
+    }
+    if (iy == 0x7f800000) return (int32_t)hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+    const int32_t k = ((int32_t)iy - (int32_t)ix) >> 23;
+    float z;
+    if (k > 60) z = pi_o_2 - u2f(0x333bbd2e);           // pi_o_2 + 0.5 pi_lo, folded
+    else if ((int32_t)hx < 0 && k < -60) z = 0.0f;
+    else z = glibc_atanf(__builtin_fabsf(y / x));
+    switch (m) {
+    case 0: return z;
+    case 1: return u2f(f2u(z) ^ 0x80000000u);
+    case 2: return pi - (z - pi_lo);
+    default: return (z - pi_lo) - pi;
+    }
+}
+
+// fdlibm e_acosf.c as glibc builds it
+BB_HD float glibc_acosf(float x)
+{
+    const float pi = u2f(0x40490fda), pio2_hi = u2f(0x3fc90fda), pio2_lo = u2f(0x33a22168);
+    const float pS0 = u2f(0x3e2aaaab), pS1 = u2f(0xbea6b090), pS2 = u2f(0x3e4e0aa8), pS3 = u2f(0xbd241146),
+                pS4 = u2f(0x3a4f7f04), pS5 = u2f(0x3811ef08);
+    const float qS1 = u2f(0xc019d139), qS2 = u2f(0x4001572d), qS3 = u2f(0xbf303361), qS4 = u2f(0x3d9dc62e);
+    const uint32_t hx = f2u(x), ix = hx & 0x7fffffff;
+    if (ix == 0x3f800000) return (int32_t)hx > 0 ? 0.0f : pi + u2f(0x34222168);  // pi + 2 pio2_lo
+    if (ix > 0x3f800000) return (x - x) / (x - x);
+    if (ix < 0x3f000000) {  // |x| < 0.5
+        if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+        const float z = x * x;
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const float r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    }
+    if ((int32_t)hx < 0) {  // x < -0.5
+        const float z = (1.0f + x) * 0.5f;
+        const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+        const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+        const float s = __builtin_sqrtf(z);
+        const float r = p / q;
+        const float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    }
+    const float z = (1.0f - x) * 0.5f;  // x > 0.5
+    const float s = __builtin_sqrtf(z);
+    const float df = u2f(f2u(s) & 0xfffff000u);
+    const float c = (z - df * df) / (s + df);
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    const float w = r * s + c;
+    return 2.0f * (df + w);
+}
+
+BB_HD float sinf_(float x) { return glibc_sincosf_one(x, false); }
+BB_HD float cosf_(float x) { return glibc_sincosf_one(x, true); }
 BB_HD void sincosf_(float x, float *s, float *c)
 {
-    double sd, cd;
-    sincos_d((double)x, &sd, &cd);
-    *s = (float)sd; *c = (float)cd;
+    *s = glibc_sincosf_one(x, false);
+    *c = glibc_sincosf_one(x, true);
 }
-BB_HD float atan2f_(float y, float x) { return (float)atan2_d((double)y, (double)x); }
-BB_HD float atanf_(float x) { return (float)atan_d((double)x); }
-BB_HD float acosf_(float x) { return (float)acos_d((double)x); }
+BB_HD float atan2f_(float y, float x) { return glibc_atan2f(y, x); }
+BB_HD float atanf_(float x) { return glibc_atanf(x); }
+BB_HD float acosf_(float x) { return glibc_acosf(x); }
 BB_HD float sqrtf_(float x) { return __builtin_sqrtf(x); }
 
 }  // namespace bbm

@@ -176,9 +176,11 @@ typedef struct {
     uint32_t flags;
     OWorld *w;
     float *obs_store;
+    int64_t ev[OR_NUM_EVENTS];      /* cumulative event counts (test coverage) */
 } Oracle;
 
-static const Oracle *G; /* current oracle (single-threaded checker) */
+static Oracle *G; /* current oracle (single-threaded checker) */
+#define EV(k) (G->ev[(k)]++)
 
 static float sample_uniform(OWorld *w, float lo, float hi) /* helper.cpp:8-11 */
 {
@@ -312,8 +314,10 @@ static void reset_world(OWorld *w) /* gen.cpp:216-316 */
     if (g->clock <= 0.f && (float)g->one_v_one == 0.f) {
         if (g->period < 4.f || g->s0 == g->s1) {
             g->period += 1.f; g->clock = K_TIME_PER_PERIOD; g->shot = 24.f; g->live = 1; g->inbounding = 0;
+            EV(OR_EV_PERIOD_ADVANCE);
         } else {
             g->live = 0;
+            EV(OR_EV_GAME_END);
         }
     } else {
         int32_t h0 = g->h0, h1 = g->h1, ovo = g->one_v_one;
@@ -363,6 +367,7 @@ static void assign_inbounder(OWorld *w, V3 ball_pos, int32_t team, Q4 orient, in
         w->gs.inbounding = 1;
         w->gs.inb_clock = 5.f;
         if (is_oob) w->gs.oob += 1.f;
+        EV(OR_EV_INBOUND_START);
     }
 }
 
@@ -431,6 +436,7 @@ static void sys_grab(OWorld *w, OAgent *a) /* game.cpp:164-239 */
     float d = vlen(vsub(b->pos, a->pos));
     if (d <= 0.3f) {
         if ((float)w->gs.one_v_one == 1.f && (float)a->team != w->gs.poss) {
+            EV(OR_EV_DEFENDER_GRAB_RESET);
             w->reset_now = 1;
             return;
         }
@@ -438,6 +444,7 @@ static void sys_grab(OWorld *w, OAgent *a) /* game.cpp:164-239 */
             OAgent *o = &w->ag[j];
             if (o->ball_id == b->id) { o->has_ball = 0; o->ball_id = PH; o->cooldown = 62.0f; }
         }
+        EV(OR_EV_GRAB);
         a->has_ball = 1; a->ball_id = b->id;
         b->holder = a->id; b->grabbed = 1; b->in_flight = 0;
         b->vel = v3(0.f, 0.f, 0.f);
@@ -452,6 +459,7 @@ static void sys_pass(OWorld *w, OAgent *a) /* game.cpp:243-270 */
     if (a->mask[2] == 0 || a->act[4] == 0) return;
     OBall *b = &w->ball;
     if (b->holder == a->id) {
+        EV(OR_EV_PASS);
         b->grabbed = 0; b->holder = PH;
         a->has_ball = 0; a->ball_id = PH; a->im_inb = 0;
         b->vel = qrot(a->q, v3(0.f, 0.1f, 0.f));
@@ -504,7 +512,8 @@ static void sys_shoot(OWorld *w, OAgent *a) /* game.cpp:273-407 */
     OBall *b = &w->ball;
     if (b->holder == a->id) {
         int32_t spv = shot_value(pos, target);
-        if (going == 1.f) { b->going_in = 1; w->gs.baskets += 1.f; }
+        EV(OR_EV_SHOT);
+        if (going == 1.f) { b->going_in = 1; w->gs.baskets += 1.f; EV(OR_EV_SHOT_GOING_IN); }
         else a->reward -= 1.f;
         b->grabbed = 0; b->holder = PH;
         a->has_ball = 0; a->ball_id = PH; a->im_inb = 0;
@@ -560,6 +569,7 @@ static void sys_score(OWorld *w, OHoop *h) /* game.cpp:873-953 */
     if (d <= h->radius && (float)b->in_flight == 1.f) {
         int32_t pts = b->shot_value;
         int32_t inb_team = 0;
+        EV(OR_EV_MAKE);
         for (int j = 0; j < G->n; j++) {
             OAgent *a = &w->ag[j];
             if (a->def_hoop == h->id) inb_team = a->team;
@@ -605,10 +615,12 @@ static void sys_out_of_bounds(OWorld *w) /* game.cpp:1055-1113 */
         if ((float)g->one_v_one == 1.f) {
             w->ag[offense_agent_index(w)].reward -= 100.f;
             w->reset_now = 1;
+            EV(OR_EV_OOB_1V1);
         } else {
             b->in_flight = 0;
             b->vel = v3(0.f, 0.f, 0.f);
             g->live = 0;
+            EV(OR_EV_OOB_TURNOVER);
             int32_t new_team = 1 - b->last_team;
             for (int i = 0; i < G->n; i++) {
                 OAgent *a = &w->ag[i];
@@ -641,6 +653,7 @@ static void sys_clock(OWorld *w) /* game.cpp:992-1030 */
     if (g->clock <= 0.f && (float)g->live > 0.5f) {
         w->ag[offense_agent_index(w)].reward += 10.f;
         w->reset_now = 1;
+        EV(OR_EV_CLOCK_EXPIRY);
     }
     if (g->shot < 0.f) g->shot = 0.f;
 }
@@ -653,6 +666,7 @@ static void sys_inbound_violation(OWorld *w) /* game.cpp:1116-1157 */
     int32_t new_team = 1 - cur;
     int32_t turn_id = PH;
     g->live = 0;
+    EV(OR_EV_INBOUND_VIOLATION);
     for (int i = 0; i < G->n; i++) {
         OAgent *a = &w->ag[i];
         if ((float)a->im_inb > 0.5f) {
@@ -674,6 +688,7 @@ static void sys_inbound_violation(OWorld *w) /* game.cpp:1116-1157 */
 static void sys_reset(OWorld *w) /* game.cpp:957-967 */
 {
     if (w->reset_now == 0) return;
+    EV(OR_EV_WORLD_RESET);
     reset_world(w);
     w->reset_now = 0;
 }
@@ -725,7 +740,9 @@ static void sys_collision(OWorld *w, OAgent *a) /* game.cpp:537-648 */
             if (ov < min_ov) { min_ov = ov; mtv = axes[j]; }
         }
         if (colliding) {
+            EV(OR_EV_CONTACT);
             if (w->gs.poss == (float)a->team) {
+                EV(OR_EV_TAG);
                 a->reward -= 10.f;
                 bb->reward += 10.f;
                 w->reset_now = 1;
@@ -882,6 +899,7 @@ static void sys_fill_obs(OWorld *w, int ai)
             if (opps < max_opps) { put_other(&s, o, a->pos, dfn, b->pos); opps++; }
         }
     }
+    if (mates < max_mates || opps < max_opps) EV(OR_EV_OBS_PADDED_ROW);
     for (int i = mates; i < max_mates; i++) for (int j = 0; j < 37; j++) put(&s, 0.f);
     for (int i = opps; i < max_opps; i++) for (int j = 0; j < 37; j++) put(&s, 0.f);
     for (int i = 0; i < n; i++) put(&s, (w->ag[i].id == b->holder) ? 1.f : 0.f);
@@ -1130,6 +1148,12 @@ int32_t oracle_shot_point_value(float px, float py, float pz, float hx, float hy
 {
     init_court();
     return shot_value(v3(px, py, pz), v3(hx, hy, hz));
+}
+
+void oracle_events(void *h, int64_t out[OR_NUM_EVENTS])
+{
+    Oracle *o = (Oracle *)h;
+    for (int k = 0; k < OR_NUM_EVENTS; k++) out[k] = o->ev[k];
 }
 
 void oracle_rotate_vec(const float q[4], const float v[3], float out[3])

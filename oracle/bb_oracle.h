@@ -71,6 +71,30 @@ void oracle_import(void *h, int32_t id, const void *in);
 void oracle_random_actions(void *h, uint32_t seed, uint32_t step);
 /* Timed loop used by bench.py's cpu_baseline leg; returns wall seconds. */
 double oracle_run_random(void *h, int32_t steps, uint32_t seed, uint32_t step0);
+/* Cumulative event counts since creation: which rare branches a run went
+ * through (coverage assertions of the parity tests). */
+enum {
+    OR_EV_SHOT = 0,            /* holder released a shot (shootSystem, game.cpp:273-407) */
+    OR_EV_SHOT_GOING_IN,       /* ... on a going-in line */
+    OR_EV_MAKE,                /* scoreSystem hit (game.cpp:873-953) */
+    OR_EV_OOB_1V1,             /* 1v1 out of bounds: -100 + reset (game.cpp:1055-1113) */
+    OR_EV_OOB_TURNOVER,        /* full-game out-of-bounds turnover (game.cpp:1083-1111) */
+    OR_EV_TAG,                 /* contact against the possessing team (game.cpp:537-648) */
+    OR_EV_CONTACT,             /* any SAT contact */
+    OR_EV_INBOUND_START,       /* assignInbounder assigned an agent (game.cpp:14-53) */
+    OR_EV_INBOUND_VIOLATION,   /* 5-s inbound violation (game.cpp:1116-1157) */
+    OR_EV_PERIOD_ADVANCE,      /* end-of-period branch of resetWorld (gen.cpp:221-236) */
+    OR_EV_GAME_END,            /* game-over branch of resetWorld (gen.cpp:221-236) */
+    OR_EV_WORLD_RESET,         /* resetSystem ran resetWorld (game.cpp:957-967) */
+    OR_EV_CLOCK_EXPIRY,        /* clockSystem +10 and reset (game.cpp:992-1030) */
+    OR_EV_GRAB,                /* grab / steal picked up the ball (game.cpp:164-239) */
+    OR_EV_PASS,                /* pass released the ball (game.cpp:243-270) */
+    OR_EV_DEFENDER_GRAB_RESET, /* 1v1 defender grab -> reset (game.cpp:164-239) */
+    OR_EV_OBS_PADDED_ROW,      /* observation row with empty mate/opponent slots (game.cpp:1428-1437) */
+    OR_NUM_EVENTS
+};
+void oracle_events(void *h, int64_t out[OR_NUM_EVENTS]);
+
 /* Exposed primitives for known-answer tests. */
 void oracle_threefry2x32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1, uint32_t out[2]);
 int32_t oracle_shot_point_value(float px, float py, float pz, float hx, float hy, float hz);

@@ -32,6 +32,13 @@ FLAG_FULL_GAME = 0x4
 MATH_CR = 0
 MATH_LIBM = 1
 
+# Cumulative event counters (bb_oracle.h OR_EV_*), in enum order.
+EVENTS = [
+    "shot", "shot_going_in", "make", "oob_1v1", "oob_turnover", "tag", "contact", "inbound_start",
+    "inbound_violation", "period_advance", "game_end", "world_reset", "clock_expiry", "grab", "pass",
+    "defender_grab_reset", "obs_padded_row",
+]
+
 
 def obs_width(n: int) -> int:
     used = 61 + 38 * (n - 1) + 2 * n
@@ -90,6 +97,7 @@ def lib():
         L.oracle_export_bytes.restype = ctypes.c_int64
         L.oracle_export_bytes.argtypes = [ctypes.c_void_p, ctypes.c_int32]
         L.oracle_random_actions.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32]
+        L.oracle_events.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)]
         L.oracle_run_random.restype = ctypes.c_double
         L.oracle_run_random.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32]
         L.oracle_threefry2x32.argtypes = [ctypes.c_uint32] * 4 + [ctypes.POINTER(ctypes.c_uint32)]
@@ -114,7 +122,7 @@ ENV_START_Y = float(np.float32(16.764000000000003 / 2.0))
 
 class Oracle:
     def __init__(self, num_worlds: int, num_agents: int = 2, seed: int = 0, flags: int = 0,
-                 world_offset: int = 0, math_mode: int = MATH_CR,
+                 world_offset: int = 0, math_mode: int = MATH_LIBM,
                  discrete_x: int = ENV_DISCRETE_X, discrete_y: int = ENV_DISCRETE_Y,
                  start_x: float = ENV_START_X, start_y: float = ENV_START_Y):
         self.n = num_agents
@@ -154,6 +162,12 @@ class Oracle:
 
     def run_random(self, steps: int, seed: int, step0: int = 0) -> float:
         return lib().oracle_run_random(self._h, steps, seed, step0)
+
+    def events(self) -> dict:
+        """Cumulative counts of the rare branches taken since creation."""
+        out = (ctypes.c_int64 * len(EVENTS))()
+        lib().oracle_events(self._h, out)
+        return {k: int(out[i]) for i, k in enumerate(EVENTS)}
 
     def snapshot(self, names=None) -> dict:
         names = names or list(EXPORTS)

@@ -1,0 +1,70 @@
+"""gfx950 kernels vs the oracle in the reference CPU executor's math mode.
+
+The reference's CPU TaskGraph executor evaluates its float transcendentals
+with glibc's float functions: std::atan2 (src/game.cpp:302), sinf/cosf
+(game.cpp:345), std::sin/std::cos on floats (game.cpp:435), std::atan
+(game.cpp:806), acosf (src/helper.cpp:39), cosf/sinf (helper.cpp:135-136).
+The product restates those glibc algorithms (csrc/bb_math.h, equal to the
+host libm on every float input, tests/test_math.py).  Here the oracle runs in
+MATH_LIBM mode -- the literal glibc float calls, i.e. the reference CPU
+executor's arithmetic -- and the HIP path must meet the north_star bar against
+it (BASELINE.json): integer / score / done state bit-exact, floats within 1e-5
+(tests/helpers.py), for identical action sequences.  Since bb_math.h restates
+glibc's float functions operation for operation, the columns are in fact
+asserted bit-identical.
+
+Each case reports the bit-identical fraction of every column (printed, and
+collected into gpurun_out/libm_parity.json when that directory exists).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from madrona_basketball_amd import ExecMode
+from oracle.oracle import MATH_LIBM, Oracle
+from tests.helpers import make_sim, oracle_flags, run_lockstep, sparse_actions
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "random_8192x1000": dict(W=8192, steps=1000),
+    "tag_heavy_4096x800": dict(W=4096, steps=800, sparse=True),
+    "no_tag_mask_2048x800": dict(W=2048, steps=800, flags=dict(tag_mask=False)),
+    "full_game_2048x800": dict(W=2048, steps=800, flags=dict(one_on_one=False)),
+    "full_game_no_tag_mask_2048x800": dict(W=2048, steps=800, flags=dict(one_on_one=False, tag_mask=False)),
+    "agents4_1000x600": dict(W=1000, steps=600, n=4),
+    "agents10_1000x400": dict(W=1000, steps=400, n=10),
+}
+
+OUT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu(native_lib, oracle_lib):
+    assert torch.cuda.is_available(), "GPU tests selected but no HIP device is visible"
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_gpu_vs_reference_cpu_math(case):
+    c = CASES[case]
+    W, steps, n = c["W"], c["steps"], c.get("n", 2)
+    flags = c.get("flags", {})
+    sim = make_sim(ExecMode.CUDA, W, num_agents=n, per_world_rng=True, **flags)
+    o = Oracle(W, num_agents=n, flags=oracle_flags(per_world_rng=True, **flags), math_mode=MATH_LIBM)
+    worst = run_lockstep(sim, o, steps, check_every=50,
+                         actions_fn=sparse_actions(o) if c.get("sparse") else None)
+    ev = o.events()
+    assert ev["world_reset"] > 0, ev
+    # beyond the north_star tolerance: bb_math.h restates glibc's float
+    # functions exactly, so every word of every column is expected identical
+    assert min(worst.values()) == 1.0, {k: v for k, v in worst.items() if v < 1.0}
+    report = {"case": case, "worlds": W, "steps": steps, "agents": n, "flags": flags,
+              "bit_identical_fraction_min_over_checks": worst,
+              "events": {k: v for k, v in ev.items() if v}}
+    print(json.dumps(report))
+    if os.path.isdir(OUT):
+        with open(os.path.join(OUT, "libm_parity.jsonl"), "a") as f:
+            f.write(json.dumps(report) + "\n")
