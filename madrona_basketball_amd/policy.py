@@ -55,6 +55,27 @@ def make_agent(seed: int = 0) -> torch.nn.Module:
     return m
 
 
+def agent_from_state_dict(state_dict: dict, device=None) -> torch.nn.Module:
+    """A module of the reference Agent's layout holding `state_dict` -- the
+    keys Agent.state_dict() / a checkpoint written by scripts/ppo.py has
+    (backbone.{0,1,3,4}.*, actor.*, critic.*, obs_norm.mean/var; the
+    value_norm / count buffers are not used by inference).  Load checkpoints
+    with torch.load(path, weights_only=True), as Agent.load does
+    (scripts/agent.py:180-182)."""
+    m = make_agent(0)
+    own = m.state_dict()
+    missing = [k for k in own if k not in state_dict]
+    if missing:
+        raise KeyError(f"state_dict lacks {missing}")
+    with torch.no_grad():
+        for k, v in own.items():
+            src = torch.as_tensor(state_dict[k])
+            if tuple(src.shape) != tuple(v.shape):
+                raise ValueError(f"{k}: shape {tuple(src.shape)}, expected {tuple(v.shape)}")
+            v.copy_(src.to(v.dtype))
+    return m if device is None else m.to(device)
+
+
 class FusedPolicy:
     def __init__(self, device: torch.device):
         self.device = torch.device(device)
