@@ -63,6 +63,35 @@ def cpu_baseline(num_agents: int, seconds: float, procs: int):
                       f"threefry random actions, ~{seconds:.0f} s per process, rates summed"}
 
 
+def _executor_worker(job):
+    """The product's own CPU executor (ExecMode.CPU, bb_host.hip: `threads`
+    std::threads over contiguous world ranges) on the same workload."""
+    num_agents, seconds, worlds, threads = job
+    os.environ["BB_CPU_THREADS"] = str(threads)
+    import madrona_basketball_amd as mba
+    sim = mba.SimpleGridworldSimulator(
+        discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
+        max_episode_length=39600, exec_mode=mba.ExecMode.CPU, num_worlds=worlds, gpu_id=-1,
+        num_agents=num_agents, per_world_rng=True)
+    sim.step_n(3, random_actions=True, action_seed=321, step0=0)  # warm
+    steps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        sim.step_n(5, random_actions=True, action_seed=321, step0=3 + steps)
+        steps += 5
+    return worlds, steps, time.perf_counter() - t0
+
+
+def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
+    """The product's CPU executor in a child process (spawned before this
+    process touches the GPU)."""
+    import multiprocessing as mp
+    worlds = 16384
+    with mp.get_context("spawn").Pool(1) as pool:
+        w, st, el = pool.apply(_executor_worker, ((num_agents, seconds, worlds, threads),))
+    return {"value": w * st / el, "unit": "env-steps/s", "cores": threads, "kind": "product host executor",
+            "sample": f"{w} worlds x {st} steps on {threads} threads, {num_agents} agents, threefry random actions"}
+
+
 def load_traffic(workload_key: str):
     """HBM bytes per step-kernel launch from the committed PMC passes
     (tools/traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
@@ -96,14 +125,17 @@ def main():
                          "into the action tensor, then the step (env.py + ppo.py's inference, on the device)")
     ap.add_argument("--no-record", action="store_true",
                     help="diagnostics: rollouts without recorded outputs (each step rewrites the sim's own tensors)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end leg (env.py's step through Python: slice write, step, 3 clones)")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    cpu = None
-    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.agents, args.cpu_seconds, args.cpu_procs)  # before any GPU call
+    cpu = cpu_exec = None
+    if rank == 0 and not args.no_cpu_baseline:  # before any GPU call (the other ranks wait at init)
+        cpu = cpu_baseline(args.agents, args.cpu_seconds, args.cpu_procs)
+        cpu_exec = cpu_executor_baseline(args.agents, min(args.cpu_seconds, 8.0), args.cpu_procs)
 
     import torch
     import torch.distributed as dist
@@ -208,6 +240,38 @@ def main():
         avg_kernel_s = elapsed / launches
     del staged
 
+    # end-to-end leg (scripts/run.py:10-15 over scripts/env.py:147,167-170):
+    # per step the trainee's int64 action rows are written into the action
+    # tensor by a torch slice assignment, SimpleGridworldSimulator.step() is
+    # called from Python, and obs / reward / done of the trainee are cloned
+    e2e = None
+    if not args.no_e2e and not args.policy and not K:
+        import torch
+        views = {k: getattr(sim, k)().to_torch() for k in
+                 ("action_tensor", "observations_tensor", "reward_tensor", "done_tensor")}
+        trainee = sim.stage_random_actions(args.steps, action_seed=args.seed,
+                                           step0=args.warmup + 2 * args.steps)[:, :, 0].to(torch.int64)
+        acts, obs_t, rew_t, done_t = (views[k] for k in ("action_tensor", "observations_tensor",
+                                                          "reward_tensor", "done_tensor"))
+        barrier()
+        t0 = time.perf_counter()
+        for t in range(args.steps):
+            acts[:, 0] = trainee[t]
+            sim.step()
+            obs_t[:, 0].detach().clone()
+            rew_t[:, 0].detach().clone()
+            done_t[:, 0].detach().clone()
+        sync()
+        e2e_s = time.perf_counter() - t0
+        barrier()
+        e2e_s = max_over_ranks(e2e_s)
+        del trainee
+        e2e = {"value": W * world_size * args.steps / e2e_s, "unit": "env-steps/s",
+               "ms_per_step": e2e_s * 1e3 / args.steps,
+               "harness": "scripts/run.py loop over env.step(): int64 trainee actions -> actions[:, 0] "
+                          "(env.py:147), SimpleGridworldSimulator.step() via ctypes, obs/reward/done "
+                          "[:, 0].clone() (env.py:167-170); agent 1 acts through the hard-coded defence"}
+
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
     L = _lib.load()
@@ -236,8 +300,10 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"{W} worlds per GPU x {args.agents} agents (reference 1v1 game, "
-                        f"NUM_AGENTS={args.agents}), threefry random actions per step (buckets "
+            "workload": f"{W} worlds per GPU x {args.agents} agents ("
+                        + ("reference 1v1 game, NUM_AGENTS=2" if args.agents == 2 else
+                           f"extension: the reference game rules with NUM_AGENTS={args.agents}, obs row "
+                           f"{L.bb_obs_width(args.agents)} floats") + "), threefry random actions per step (buckets "
                         f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
                         + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
                            f"of every step recorded into [{K}, W, N, ...] buffers" if K else "; one step per call")
@@ -265,9 +331,11 @@ def main():
         out["config"]["parallelism"] += " (host executor, gloo)"
     if args.policy:
         out["roofline"] = None  # several kernels per step: see the rocprof summary
+    if e2e is not None:
+        out["e2e"] = e2e
     if rank == 0:
         out["cpu_baseline"] = cpu
-    if rank == 0:
+        out["cpu_executor"] = cpu_exec
         print(json.dumps(out), flush=True)
     if world_size > 1:
         dist.destroy_process_group()

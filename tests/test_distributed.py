@@ -33,7 +33,7 @@ def test_bench_two_ranks_gloo():
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1", BB_CPU_THREADS="2")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--exec", "cpu", "--worlds", "512", "--steps", "20", "--warmup", "2", "--no-cpu-baseline"]
+           "--gpus", "2", "--exec", "cpu", "--worlds", "512", "--steps", "20", "--warmup", "2", "--cpu-seconds", "0.5", "--cpu-procs", "1"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -41,6 +41,9 @@ def test_bench_two_ranks_gloo():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["total_worlds"] == 1024 and out["value"] > 0
     assert out["scaling"] == "weak" and out["steps"] == 20
+    # the CPU baselines ride on multi-rank lines too (rank 0, before any device call)
+    assert out["cpu_baseline"]["value"] > 0 and out["cpu_executor"]["value"] > 0
+    assert out["e2e"]["value"] > 0  # the env.py loop, max over ranks
 
 
 def _worker(rank, world, port, W, steps, q):

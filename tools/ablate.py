@@ -38,8 +38,15 @@ def main():
                                        num_agents=args.agents, per_world_rng=True)
     sim.step_n(50, random_actions=True)  # realistic, diverged state
     torch.cuda.synchronize()
-    B = L.bb_algorithmic_bytes_per_world(args.agents)
-    read_q, write_q = 28, (B * 0 + 1256 + 15) // 16
+    N = args.agents
+    B = L.bb_algorithmic_bytes_per_world(N)
+    obs_b = N * 4 * (61 + 38 * (N - 1) + 2 * N)  # observation bytes of B
+    reads = N * 144 + 120                          # per-agent and per-world reads of B
+    # the probe moves B in 16-byte pieces: its reads, then the rest as writes
+    read_q, write_q = (reads + 15) // 16, (B - reads + 15) // 16
+    # algorithmic bytes each mode moves per world: the variants without the
+    # observation pass do not write the rows, the probe moves its own pieces
+    moved = {0: B, 1: B - obs_b, 2: B, 3: B, 4: B - obs_b, 100: 16 * (read_q + write_q)}
     modes = {m: MODES[m] for m in (args.only if args.only is not None else MODES)}
     res = {m: [] for m in modes}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -52,9 +59,13 @@ def main():
     out = {}
     for m, v in res.items():
         med = statistics.median(v)
-        out[MODES[m]] = {"median_us": med, "min_us": min(v), "algorithmic_GBps": B * args.worlds / (med * 1e-6) / 1e9}
+        gbs = moved[m] * args.worlds / (med * 1e-6) / 1e9
+        out[MODES[m]] = {"median_us": med, "min_us": min(v), "bytes_per_world": moved[m], "GBps": gbs}
+        # above the HBM peak the bytes did not all come from / go to HBM
+        # (Infinity-Cache-resident state): say so instead of quoting a rate
+        note = "  (> 8 TB/s HBM peak: cache-resident, not an HBM rate)" if gbs > 8000 else ""
         print(f"{MODES[m]:40s} median {med:8.2f} us  min {min(v):8.2f} us  "
-              f"alg {out[MODES[m]]['algorithmic_GBps']:7.0f} GB/s", flush=True)
+              f"{moved[m]:6d} B/world  {gbs:7.0f} GB/s{note}", flush=True)
     if args.only is None:
         out["trace"] = trace(L, sim, stream)
     print(json.dumps({"worlds": args.worlds, "agents": args.agents, "results": out}))
