@@ -18,6 +18,7 @@
 // step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <type_traits>
 #include "bb_launch.h"
 #include "bb_sim.h"
 
@@ -107,6 +108,14 @@ struct PhasedTile {
 // where the 416 written bytes of 2 x 13 pieces are cheaper.
 template <int N>
 using RolloutTile = PhasedTile<N, 128, 16>;
+
+// k_step's tile.  LINES (state beyond the Infinity Cache): whole 128-byte
+// lines per pass, zero tail included, like k_rollout -- at 262 144 worlds
+// 99.3 -> 88.0 us per step (partial lines reach HBM as partial writes);
+// otherwise 2 x 13 pieces (416 written bytes per row), cheaper while the rows
+// stay cache-resident (65 536 worlds: 21.95 vs 22.14 us).
+template <int N, bool LINES>
+using StepTile = typename std::conditional<LINES, RolloutTile<N>, PhasedTile<N>>::type;
 
 // RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
 // Indices are compile-time after unrolling, so the window test folds away and
@@ -371,10 +380,10 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
 }
 
 // One lane per agent: lane = (w - w0) * N + k.
-template <int N, int MODE>
+template <int N, int MODE, bool LINES>
 __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 {
-    constexpr int OW = obs_width(N);
+    using T = StepTile<N, LINES>;
     const int lane = threadIdx.x;
     const int k = lane % N;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
@@ -389,7 +398,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     // The event-only words as loaded (store only on change, see Orig) wait
     // in the lane's row of the observation tile, which is free until the
     // observation pass: registers stay with the systems.
-    LaneOrig *lo = (LaneOrig *)(tile + lane * PhasedTile<N>::RS);
+    LaneOrig *lo = (LaneOrig *)(tile + lane * T::RS);
     if (active) {
         load_world(s, p, w);
         {
@@ -423,7 +432,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 
     const int32_t ib = active ? inbounder_id(s) : -1;
     const bool share = active && obs_sharable(s);
-    agent_lane_obs<N, MODE>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+    agent_lane_obs<N, MODE, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
     trace_point<MODE>(p, 9);
 }
 
@@ -556,11 +565,19 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
 // world-level systems on it together (same instructions, same values); the
 // per-agent systems are computed by the agent's lane and exchanged through
 // an LDS buffer (LdsAgents).  No per-lane copy of the world: nothing to spill.
-#ifndef BB_XW
-#define BB_XW 33
+#ifndef BB_OBS_PIECES
+#define BB_OBS_PIECES 1
 #endif
-// Words per lane in the exchange buffer (>= Intrinsic).  Odd, so that the
-// rows lanes of different worlds read at once fall in different LDS banks
+#ifndef BB_SHARED_TILE
+#define BB_SHARED_TILE 0
+#endif
+#ifndef BB_XW
+#define BB_XW ((BB_OBS_PIECES && !BB_SHARED_TILE) ? 13 : 33)
+#endif
+// Words per lane in the exchange buffer (>= the systems' per-agent results;
+// >= Intrinsic where the observation pass exchanges intrinsic blocks through
+// it).  Odd, so that the rows lanes of different worlds read at once fall in
+// different LDS banks
 // (at 32 words the row start is 0 or 32 mod 64 banks: up to 30-way conflicts).
 constexpr int XW = BB_XW;
 
@@ -583,12 +600,182 @@ struct LdsAgents {
     __device__ void mark(int point) const { trace_point<MODE>(*p, point); }
 };
 
+// ---- observation rows as whole-wave pieces (N >= 4) -------------------------
+// A wave's WPW worlds own WPW*N consecutive observation rows.  After the
+// systems, each world's lanes write the row *sources* into an LDS table
+// (ObsSrc, overlaying the then dead world state and exchange buffer): the two
+// team contexts (obs 0-22), every agent's position and intrinsic block, the
+// observer-to-agent direction/distance matrix and the one-hot tails.  A
+// per-float decode table (PieceCode, row position i -> table entry as a
+// function of the observer a) lets the wave write its rows as consecutive
+// 16-byte pieces -- 1 KB of whole lines per store instruction instead of one
+// 16-byte piece of each of 64 rows -- every float bit-identical to
+// emit_row_view.  Only worlds whose rows share the intrinsic blocks
+// (obs_sharable: every generated world) take this path.
+template <int N>
+struct ObsSrc {
+    static constexpr int QR = obs_width(N) / 4;   // 16-byte pieces per row
+    static constexpr int CTX = 0;                 // [2][23] context of a team-0 / team-1 observer
+    static constexpr int PI = 46;                 // [N][34] position (3) + intrinsic block (31)
+    static constexpr int R = PI + 34 * N;         // [N][N-1][4] direction (3) + distance a -> j, j != a
+    static constexpr int OH = R + 4 * N * (N - 1);  // [2N] holder one-hot, inbounder one-hot
+    static constexpr int TM = OH + 2 * N;         // [N] team(a) != 0 (int bits)
+    static constexpr int Z = TM + N;              // one zero
+    static constexpr int ES = (Z + 1) | 1;        // floats per world (odd: worlds in different banks)
+};
+
+// code[i] for row float i: entry = base + MA*a + MJ*(T ? t : j) + MT*team(a),
+// with j = t + (t >= a) the agent in other-agent block t of observer a:
+// bits 0-9 base, 10-15 MA, 16-21 MJ, 22-26 MT, 27 T, 28-31 t.
+template <int N>
+struct PieceCode {
+    uint32_t c[obs_width(N)];
+};
+template <int N>
+constexpr uint32_t piece_code(int i)
+{
+    using S = ObsSrc<N>;
+    static_assert(S::Z < 1024 && 4 * (N - 1) < 64 && N <= 16, "code fields");
+    const int tail = 61 + 38 * (N - 1);
+    auto code = [](int base, int ma, int mj, int mt, int t, int tsel = 0) {
+        return (uint32_t)base | ((uint32_t)ma << 10) | ((uint32_t)mj << 16) | ((uint32_t)mt << 22)
+               | ((uint32_t)tsel << 27) | ((uint32_t)t << 28);
+    };
+    if (i < 23) return code(S::CTX + i, 0, 0, 23, 0);
+    if (i < 26) return code(S::PI + (i - 23), 34, 0, 0, 0);
+    if (i < 30) return code(S::Z, 0, 0, 0, 0);
+    if (i < 61) return code(S::PI + 3 + (i - 30), 34, 0, 0, 0);
+    if (i < tail) {
+        const int u = i - 61, t = u / 38, f = u % 38;
+        if (f < 3) return code(S::PI + f, 0, 34, 0, t);
+        if (f < 7) return code(S::R + (f - 3), 4 * (N - 1), 4, 0, t, 1);  // row a, column t
+        return code(S::PI + 3 + (f - 7), 0, 34, 0, t);
+    }
+    if (i < tail + 2 * N) return code(S::OH + (i - tail), 0, 0, 0, 0);
+    return code(S::Z, 0, 0, 0, 0);
+}
+template <int N>
+constexpr PieceCode<N> make_piece_code()
+{
+    PieceCode<N> m{};
+    for (int i = 0; i < obs_width(N); i++) m.c[i] = piece_code<N>(i);
+    return m;
+}
+template <int N>
+__constant__ PieceCode<N> PIECE_CODE = make_piece_code<N>();
+
+template <int N>
+__device__ __forceinline__ int piece_src(uint32_t code, int a, int tm)
+{
+    const int t = (int)(code >> 28);
+    const int j = ((code >> 27) & 1u) ? t : t + (t >= a ? 1 : 0);
+    return (int)(code & 0x3FFu) + (int)((code >> 10) & 0x3Fu) * a + (int)((code >> 16) & 0x3Fu) * j
+           + (int)((code >> 22) & 0x1Fu) * tm;
+}
+
 template <int N>
 struct SharedLds {
     static constexpr int WPW = WAVE / N;  // worlds per wave
-    World<N> world[WPW];
-    uint32_t x[WAVE][XW];
+    union {
+        struct {
+            World<N> world[WPW];
+            uint32_t x[WAVE][XW];              // systems: per-agent exchange
+        };
+        float e[WPW][ObsSrc<N>::ES];           // observation pass: row sources
+    };
+    uint4 code[BB_OBS_PIECES ? obs_width(N) / 4 : 1];  // PieceCode, 4 codes per piece
 };
+
+// The lane's sources (agent k of its world), computed from the world state
+// into registers; written into the table by put() once every lane is done
+// reading the state the table overlays.  Position and intrinsic block
+// always (the direct row of a non-sharable world reads them too).
+template <int N>
+struct LaneSources {
+    float pi[34];
+    float r[N][4];
+    float ctx[23];
+    float oh_holder, oh_inb;
+    int32_t tm;
+    bool first;  // lowest agent of its team: writes the team's context
+
+    __device__ __forceinline__ void compute(const World<N> &s, const Ctx &c, int k, int32_t ib, bool share)
+    {
+        {
+            ArraySink<34> o;
+            o.idx = 0;
+            o.put3(s.pos(k));
+            emit_intrinsic(s, o, k, attacking_hoop(s, c, k));
+#pragma unroll
+            for (int q = 0; q < 34; q++) pi[q] = o.v[q];
+        }
+        if (!share) return;
+        const F3 p = s.pos(k);
+#pragma unroll
+        for (int j = 0; j < N; j++) {
+            const F3 to = s.pos(j) - p;  // as emit_row_view
+            const float l2 = len2(to);
+            const float rr = 1.0f / bbm::sqrtf_(l2);
+            const F3 d = l2 > 1e-6f ? to * rr : f3(0.f, 0.f, 0.f);
+            r[j][0] = d.x; r[j][1] = d.y; r[j][2] = d.z; r[j][3] = bbm::sqrtf_(l2);
+        }
+        oh_holder = AGENT0_ID + k == s.holder ? 1.f : 0.f;
+        oh_inb = AGENT0_ID + k == ib ? 1.f : 0.f;
+        tm = s.team[k] != 0 ? 1 : 0;
+        first = true;
+#pragma unroll
+        for (int j = 0; j < N; j++) first &= !(j < k && s.team[j] == s.team[k]);
+        if (first) {
+            ArraySink<23> o;
+            o.idx = 0;
+            F3 att, dfn;
+            obs_context(s, c, o, k, &att, &dfn);
+#pragma unroll
+            for (int q = 0; q < 23; q++) ctx[q] = o.v[q];
+        }
+    }
+
+    __device__ __forceinline__ void put(float *e, int k, bool share) const
+    {
+        using S = ObsSrc<N>;
+#pragma unroll
+        for (int q = 0; q < 34; q++) e[S::PI + 34 * k + q] = pi[q];
+        if (!share) return;
+#pragma unroll
+        for (int j = 0; j < N; j++)
+            if (j != k)
+#pragma unroll
+                for (int q = 0; q < 4; q++) e[S::R + 4 * (k * (N - 1) + (j > k ? j - 1 : j)) + q] = r[j][q];
+        e[S::OH + k] = oh_holder;
+        e[S::OH + N + k] = oh_inb;
+        e[S::TM + k] = bitsf((uint32_t)tm);
+        if (first)
+#pragma unroll
+            for (int q = 0; q < 23; q++) e[S::CTX + 23 * tm + q] = ctx[q];
+        if (k == 0) e[S::Z] = 0.f;
+    }
+};
+
+// The wave's rows [row0, row0 + WPW*N) whose bit is set in `rows` as
+// consecutive 16-byte pieces: piece f = it*64 + lane.
+template <int N>
+__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
+{
+    using S = ObsSrc<N>;
+    constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, TOTAL = WPW * N * QR;
+    char *base = (char *)(obs + row0 * obs_width(N));
+    for (int f = lane; f < TOTAL; f += WAVE) {
+        const int r = f / QR, q = f - r * QR;
+        if (!((rows >> r) & 1ull)) continue;
+        const int slot = r / N, a = r - slot * N;
+        const float *e = sm.e[slot];
+        const int tm = (int)fbits(e[S::TM + a]);
+        const uint4 cd = sm.code[q];
+        const float v0 = e[piece_src<N>(cd.x, a, tm)], v1 = e[piece_src<N>(cd.y, a, tm)];
+        const float v2 = e[piece_src<N>(cd.z, a, tm)], v3 = e[piece_src<N>(cd.w, a, tm)];
+        *(vf4 *)(base + (uint32_t)f * 16u) = vf4{v0, v1, v2, v3};
+    }
+}
 
 template <int N, int MODE, int PHASE = 0>
 __device__ __forceinline__ void obs_phases_view(const World<N> &s, const Ctx &c, int k, const uint32_t (*x)[XW],
@@ -613,9 +800,6 @@ __device__ __forceinline__ void obs_phases_view(const World<N> &s, const Ctx &c,
     }
 }
 
-#ifndef BB_SHARED_TILE
-#define BB_SHARED_TILE 0
-#endif
 template <int N>
 struct SharedTiled {
     static constexpr bool value = BB_SHARED_TILE != 0;
@@ -639,6 +823,11 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     const LdsAgents<N, MODE> ag{k, slot, sm.x, &p};
     Ctx c = make_ctx(p, w, active && k == 0);
     trace_point<MODE>(p, 0);
+    constexpr bool PIECES = BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value;
+    if constexpr (PIECES) {  // the decode table into LDS (one copy per wave, L2-resident)
+        const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
+        for (int i = lane; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
+    }
 
     if (active) {
         load_world_agent(s, p, w, k);
@@ -679,10 +868,42 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     trace_point<MODE>(p, 8);
     if constexpr (MODE == MODE_IO || MODE == MODE_NO_OBS) return;
 
-    // observations: intrinsic block of the lane's agent into the exchange
-    // buffer, then the row in passes through the tile
     const int32_t ib = inbounder_id(s);
     const bool share = obs_sharable(s);
+    if constexpr (PIECES) {
+        LaneSources<N> src;
+        if (active) {
+            src.compute(s, c, k, ib, share);
+            if (!share) {  // rows the pieces do not cover: straight from the lane
+                float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
+                if (canonical_slots(s, k)) {
+                    fill_obs_fast(s, c, k, grow, ib);
+                } else {
+                    fill_obs_slow(s, c, k, grow, ib);
+                }
+            }
+        }
+        const uint64_t rows = __ballot(active && share);
+        __syncthreads();  // the world state is dead: the source table overlays it
+        if (active) src.put(sm.e[slot], k, share);
+        __syncthreads();
+        emit_pieces<N>(sm, rows, p.c.obs, w0 * N, lane);
+        trace_point<MODE>(p, 9);
+        return;
+    }
+    if constexpr (XW < INTRINSIC) {
+        // (diagnostic modes of a piece build) no room in the exchange buffer
+        // for intrinsic blocks: each lane writes its row alone
+        if (active) {
+            float *grow = p.c.obs + (w * N + k) * (int64_t)OW;
+            if (canonical_slots(s, k)) fill_obs_fast(s, c, k, grow, ib);
+            else fill_obs_slow(s, c, k, grow, ib);
+        }
+        trace_point<MODE>(p, 9);
+        return;
+    } else {
+    // observations: intrinsic block of the lane's agent into the exchange
+    // buffer, then the row in passes through the tile
     {
         ArraySink<INTRINSIC> o;
         o.idx = 0;
@@ -714,6 +935,7 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         obs_phases_view<N, MODE>(s, c, k, sm.x, slot, share, fast, tile, w0 * N, lane, ib);
     }
     trace_point<MODE>(p, 9);
+    }
 }
 
 // One lane per world.
@@ -775,11 +997,11 @@ __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 9);
 }
 
-template <int N>
+template <int N, bool LINES>
 constexpr int tile_floats()
 {
     if constexpr (Lanes<N>::SHARED) return BB_SHARED_TILE ? PhasedTile<N>::FLOATS : 4;
-    return Lanes<N>::LPW == N ? PhasedTile<N>::FLOATS : ObsTile<N>::FLOATS;
+    return Lanes<N>::LPW == N ? StepTile<N, LINES>::FLOATS : ObsTile<N>::FLOATS;
 }
 
 // Start skew (timing experiment, off by default): wave group blockIdx % G
@@ -799,16 +1021,16 @@ __device__ __forceinline__ void start_skew()
     }
 }
 
-template <int N, int MODE>
+template <int N, int MODE, bool LINES = false>
 __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
 {
-    __shared__ float4 tile4[tile_floats<N>() / 4];
+    __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
     start_skew();
     if constexpr (Lanes<N>::SHARED) {
         __shared__ SharedLds<N> sm;
         step_shared_world<N, MODE>(p, (float *)tile4, sm);
     } else if constexpr (Lanes<N>::LPW == N) {
-        step_agent_lanes<N, MODE>(p, (float *)tile4);
+        step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);
     } else {
         step_world_lanes<N, MODE>(p, (float *)tile4);
     }
@@ -824,6 +1046,16 @@ __global__ __launch_bounds__(256) void k_init(const Params p)
 
 // ev0/ev1 (optional): hipExtLaunchKernel records the kernel's own start and
 // end in them (the dispatch packet's timestamps, as rocprofv3 reports them).
+// Whole-line observation passes once a step's state and rows no longer fit
+// comfortably in the 256 MiB Infinity Cache (see StepTile).
+constexpr int64_t LINES_MIN_BYTES = 192ll << 20;
+template <int N>
+bool step_lines(int64_t num_worlds)
+{
+    const int64_t per_world = (int64_t)N * (obs_width(N) * 4 + 240) + 160;  // rows + state columns
+    return Lanes<N>::LPW == N && !Lanes<N>::SHARED && num_worlds * per_world > LINES_MIN_BYTES;
+}
+
 template <int N>
 hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
@@ -831,7 +1063,10 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
-    case MODE_FULL: BB_LAUNCH(MODE_FULL); break;
+    case MODE_FULL:
+        if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid, block, 0, s, ev0, ev1, 0, p);
+        else BB_LAUNCH(MODE_FULL);
+        break;
     case MODE_IO: BB_LAUNCH(MODE_IO); break;
     case MODE_IO_OBS: BB_LAUNCH(MODE_IO_OBS); break;
     case MODE_DIRECT_OBS: BB_LAUNCH(MODE_DIRECT_OBS); break;

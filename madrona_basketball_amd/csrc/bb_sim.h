@@ -1916,6 +1916,12 @@ BB_HD void load_world_agent(World<N> &s, const Params &p, int64_t w, int i)
     for (int k = 0; k < 4; k++) s.msk[i][k] = 0;  // rewritten by actionMaskSystem
 }
 
+// Diagnostics A/B: BB_FULL_ROWS rewrites the whole GameState and Attributes
+// rows every step (whole 64-byte segments) instead of only their changed words.
+#ifndef BB_FULL_ROWS
+#define BB_FULL_ROWS 0
+#endif
+
 // World-level columns (GameState, WorldClock, RNG counter, ball).  With `o`,
 // the event-only words are rewritten only when changed (see Orig).
 template <int N>
@@ -1924,7 +1930,7 @@ BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, con
     const Columns &c = p.c;
     uint32_t g[14];
     game_words(s, g);
-    bool game_ev = o == nullptr;
+    bool game_ev = o == nullptr || BB_FULL_ROWS;
     if (o) {
 #pragma unroll
         for (int k = 0; k < 14; k++)
@@ -1984,7 +1990,7 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
     c.cooldown[r] = s.cd[i];
     c.cur_step[r] = s.step[i];
     if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2>(c.inbounding, r, ib);
-    bool attr_ev = o == nullptr;
+    bool attr_ev = o == nullptr || BB_FULL_ROWS;
     if (o) {
 #pragma unroll
         for (int k = 0; k < 5; k++) attr_ev |= at[k] != o->attr[k];
