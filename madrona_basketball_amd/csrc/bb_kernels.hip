@@ -621,7 +621,7 @@ struct ObsSrc {
     static constexpr int OH = R + 4 * N * (N - 1);  // [2N] holder one-hot, inbounder one-hot
     static constexpr int TM = OH + 2 * N;         // [N] team(a) != 0 (int bits)
     static constexpr int Z = TM + N;              // one zero
-    static constexpr int ES = (Z + 1) | 1;        // floats per world (odd: worlds in different banks)
+    static constexpr int ES = (Z + 4) & ~3;       // floats per world (whole 4-entry groups: esw stays inside)
 };
 
 // code[i] for row float i: entry = base + MA*a + MJ*(T ? t : j) + MT*team(a),
@@ -663,6 +663,11 @@ constexpr PieceCode<N> make_piece_code()
 }
 template <int N>
 __constant__ PieceCode<N> PIECE_CODE = make_piece_code<N>();
+
+// Table entries are stored swizzled: bits 0-1 of the index XOR bits 5-6, so
+// that the 4-float stride of consecutive lanes' pieces (lane L reads entry
+// ~4L + c) spreads over all 32 banks instead of 8 (4-way conflicts).
+__device__ __forceinline__ int esw(int i) { return i ^ ((i >> 5) & 3); }
 
 template <int N>
 __device__ __forceinline__ int piece_src(uint32_t code, int a, int tm)
@@ -739,41 +744,65 @@ struct LaneSources {
     {
         using S = ObsSrc<N>;
 #pragma unroll
-        for (int q = 0; q < 34; q++) e[S::PI + 34 * k + q] = pi[q];
+        for (int q = 0; q < 34; q++) e[esw(S::PI + 34 * k + q)] = pi[q];
         if (!share) return;
 #pragma unroll
         for (int j = 0; j < N; j++)
             if (j != k)
 #pragma unroll
-                for (int q = 0; q < 4; q++) e[S::R + 4 * (k * (N - 1) + (j > k ? j - 1 : j)) + q] = r[j][q];
-        e[S::OH + k] = oh_holder;
-        e[S::OH + N + k] = oh_inb;
-        e[S::TM + k] = bitsf((uint32_t)tm);
+                for (int q = 0; q < 4; q++) e[esw(S::R + 4 * (k * (N - 1) + (j > k ? j - 1 : j)) + q)] = r[j][q];
+        e[esw(S::OH + k)] = oh_holder;
+        e[esw(S::OH + N + k)] = oh_inb;
+        e[esw(S::TM + k)] = bitsf((uint32_t)tm);
         if (first)
 #pragma unroll
-            for (int q = 0; q < 23; q++) e[S::CTX + 23 * tm + q] = ctx[q];
-        if (k == 0) e[S::Z] = 0.f;
+            for (int q = 0; q < 23; q++) e[esw(S::CTX + 23 * tm + q)] = ctx[q];
+        if (k == 0) e[esw(S::Z)] = 0.f;
     }
 };
 
-// The wave's rows [row0, row0 + WPW*N) whose bit is set in `rows` as
-// consecutive 16-byte pieces: piece f = it*64 + lane.
+// The wave's rows [row0, row0 + WPW*N) whose bit is set in `rows`, row by
+// row: lane L writes pieces L, L + 64, ... of each row (the row's bytes in 1 KB
+// of consecutive pieces per store instruction).  A lane's pieces sit at the
+// same row positions in every row, so their table entries are decoded once,
+// per observer a (the row loop is unrolled over a), before the loop: per
+// piece the loop does 4 LDS reads and one store; the row's team (obs 0-22
+// entries) is a wave-uniform offset.
 template <int N>
 __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
-    constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, TOTAL = WPW * N * QR;
-    char *base = (char *)(obs + row0 * obs_width(N));
-    for (int f = lane; f < TOTAL; f += WAVE) {
-        const int r = f / QR, q = f - r * QR;
-        if (!((rows >> r) & 1ull)) continue;
-        const int slot = r / N, a = r - slot * N;
+    constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
+    int src[NP][N][4], dtm[NP][4];
+#pragma unroll
+    for (int p = 0; p < NP; p++) {
+        const int q = p * WAVE + lane;
+        const uint4 cd = sm.code[q < QR ? q : 0];
+        const uint32_t code[4] = {cd.x, cd.y, cd.z, cd.w};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+#pragma unroll
+            for (int a = 0; a < N; a++) src[p][a][c] = esw(piece_src<N>(code[c], a, 0));
+            dtm[p][c] = esw(piece_src<N>(code[c], 0, 1)) - esw(piece_src<N>(code[c], 0, 0));  // context entries only
+        }
+    }
+    char *base = (char *)(obs + row0 * obs_width(N)) + lane * 16;
+    for (int slot = 0; slot < WPW; slot++) {
         const float *e = sm.e[slot];
-        const int tm = (int)fbits(e[S::TM + a]);
-        const uint4 cd = sm.code[q];
-        const float v0 = e[piece_src<N>(cd.x, a, tm)], v1 = e[piece_src<N>(cd.y, a, tm)];
-        const float v2 = e[piece_src<N>(cd.z, a, tm)], v3 = e[piece_src<N>(cd.w, a, tm)];
-        *(vf4 *)(base + (uint32_t)f * 16u) = vf4{v0, v1, v2, v3};
+#pragma unroll
+        for (int a = 0; a < N; a++) {
+            const int r = slot * N + a;
+            if (!((rows >> r) & 1ull)) continue;  // wave-uniform
+            const int tmask = -(int)fbits(e[esw(S::TM + a)]);  // team 1: all ones
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                if (p * WAVE + lane < QR) {
+                    const float v0 = e[src[p][a][0] + (dtm[p][0] & tmask)], v1 = e[src[p][a][1] + (dtm[p][1] & tmask)];
+                    const float v2 = e[src[p][a][2] + (dtm[p][2] & tmask)], v3 = e[src[p][a][3] + (dtm[p][3] & tmask)];
+                    *(vf4 *)(base + ((uint32_t)r * QR + p * WAVE) * 16u) = vf4{v0, v1, v2, v3};
+                }
+            }
+        }
     }
 }
 
