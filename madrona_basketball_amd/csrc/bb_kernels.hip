@@ -853,14 +853,15 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     Ctx c = make_ctx(p, w, active && k == 0);
     trace_point<MODE>(p, 0);
     constexpr bool PIECES = BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value;
-    if constexpr (PIECES) {  // the decode table into LDS (one copy per wave, L2-resident)
-        const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
-        for (int i = lane; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
-    }
 
     if (active) {
-        load_world_agent(s, p, w, k);
-        if (k == 0) load_world_shared(s, p, w);
+        // every load issued before the first LDS write (one memory latency)
+        AgentRaw<N> ar;
+        WorldRaw wr;
+        ar.load(p, w, k);
+        if (k == 0) wr.load(p, w);
+        ar.commit(s, k);
+        if (k == 0) wr.commit(s);
     }
     __syncthreads();
     // event-only words as loaded (store only on change, see Orig)
@@ -1057,6 +1058,11 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
     start_skew();
     if constexpr (Lanes<N>::SHARED) {
         __shared__ SharedLds<N> sm;
+        if constexpr (BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value) {
+            // the decode table into LDS (one copy per wave, L2-resident)
+            const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
+            for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
+        }
         step_shared_world<N, MODE>(p, (float *)tile4, sm);
     } else if constexpr (Lanes<N>::LPW == N) {
         step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);

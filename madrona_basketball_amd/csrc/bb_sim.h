@@ -1861,59 +1861,97 @@ BB_HD bool differ(const uint32_t (&a)[NW], const uint32_t (&b)[NW])
 
 // The loads of load_world split by owner, for kernels whose N lanes of a
 // world load it together (lane i: agent i's columns; lane 0 also the world's).
+// Raw words first (load), converted into the world later (commit), so a
+// kernel can issue the loads of its next world group early.
+struct WorldRaw {  // world-level columns: GameState, WorldClock, RNG counter, ball
+    uint32_t g[14], clock, rng, bp[3], bv[3], ph[7], gb[2];
+    BB_HD void load(const Params &p, int64_t w)
+    {
+        const Columns &c = p.c;
+        load_words<14>(c.game_state, w, g);
+        clock = (uint32_t)c.world_clock[w];
+        rng = c.rng_counter[w];
+        const uint32_t *b = (const uint32_t *)c.ball_pos + w * 3, *v = (const uint32_t *)c.ball_vel + w * 3;
+        const uint32_t *h = (const uint32_t *)c.ball_physics + w * 7;
+#pragma unroll
+        for (int k = 0; k < 3; k++) { bp[k] = b[k]; bv[k] = v[k]; }
+#pragma unroll
+        for (int k = 0; k < 7; k++) ph[k] = h[k];
+        load_words<2>(c.ball_grabbed, w, gb);
+    }
+    template <int N>
+    BB_HD void commit(World<N> &s) const
+    {
+        s.g_inb = (int32_t)g[0]; s.g_live = (int32_t)g[1]; s.g_period = bitsf(g[2]); s.g_poss = bitsf(g[3]);
+        s.g_h0 = (int32_t)g[4]; s.g_s0 = bitsf(g[5]); s.g_h1 = (int32_t)g[6]; s.g_s1 = bitsf(g[7]);
+        s.g_clock = bitsf(g[8]); s.g_shot = bitsf(g[9]); s.g_bask = bitsf(g[10]); s.g_oob = bitsf(g[11]);
+        s.g_inbclk = bitsf(g[12]); s.g_1v1 = (int32_t)g[13];
+        s.reset_now = (int32_t)clock;
+        s.rng_ctr = rng;
+        s.bx = bitsf(bp[0]); s.by = bitsf(bp[1]); s.bz = bitsf(bp[2]);
+        s.bvx = bitsf(bv[0]); s.bvy = bitsf(bv[1]); s.bvz = bitsf(bv[2]);
+        s.fl = (int32_t)ph[0]; s.lta = (int32_t)ph[1]; s.ltt = (int32_t)ph[2]; s.sba = (int32_t)ph[3];
+        s.sbt = (int32_t)ph[4]; s.spv = (int32_t)ph[5]; s.gin = (int32_t)ph[6];
+        s.grab = (int32_t)gb[0]; s.holder = (int32_t)gb[1];
+    }
+};
+
+template <int N>
+struct AgentRaw {  // agent i's columns (row w*N + i)
+    uint32_t a[6], pos[3], ps[3], q[4], v[3], ib[2], at[10], rst, cd, st, t0, t4;
+    BB_HD void load(const Params &p, int64_t w, int i)
+    {
+        const Columns &c = p.c;
+        const int64_t r = w * N + i;
+        load_words<6>(c.action, r, a);
+        load_words<3>(c.agent_pos, r, pos);
+        load_words<3>(c.possession, r, ps);
+        load_words<4>(c.orientation, r, q);
+        load_words<3>(c.agent_vel, r, v);
+        load_words<2>(c.inbounding, r, ib);
+        load_words<10>(c.attributes, r, at);
+        rst = (uint32_t)c.reset[r];
+        cd = fbits(c.cooldown[r]);
+        st = c.cur_step[r];
+        t0 = c.team[r * 5];
+        t4 = c.team[r * 5 + 4];
+    }
+    BB_HD void commit(World<N> &s, int i) const
+    {
+        s.rst[i] = (int32_t)rst;
+#pragma unroll
+        for (int k = 0; k < 6; k++) s.act[i][k] = (int32_t)a[k];
+        s.px[i] = bitsf(pos[0]); s.py[i] = bitsf(pos[1]); s.pz[i] = bitsf(pos[2]);
+        s.has[i] = (int32_t)ps[0]; s.bid[i] = (int32_t)ps[1]; s.pw[i] = (int32_t)ps[2];
+        s.qw[i] = bitsf(q[0]); s.qx[i] = bitsf(q[1]); s.qy[i] = bitsf(q[2]); s.qz[i] = bitsf(q[3]);
+        s.vx[i] = bitsf(v[0]); s.vy[i] = bitsf(v[1]); s.vz[i] = bitsf(v[2]);
+        s.cd[i] = bitsf(cd);
+        s.step[i] = st;
+        s.inb[i] = (int32_t)ib[0]; s.allow[i] = (int32_t)ib[1];
+#pragma unroll
+        for (int k = 0; k < 10; k++) s.attr[i][k] = bitsf(at[k]);
+        s.team[i] = (int32_t)t0;
+        s.dhoop[i] = (int32_t)t4;
+        s.rew[i] = 0.f; s.done[i] = 0.f;  // rewritten by tick before any read
+#pragma unroll
+        for (int k = 0; k < 4; k++) s.msk[i][k] = 0;  // rewritten by actionMaskSystem
+    }
+};
+
 template <int N>
 BB_HD void load_world_shared(World<N> &s, const Params &p, int64_t w)
 {
-    const Columns &c = p.c;
-    uint32_t g[14];
-    load_words<14>(c.game_state, w, g);
-    s.g_inb = (int32_t)g[0]; s.g_live = (int32_t)g[1]; s.g_period = bitsf(g[2]); s.g_poss = bitsf(g[3]);
-    s.g_h0 = (int32_t)g[4]; s.g_s0 = bitsf(g[5]); s.g_h1 = (int32_t)g[6]; s.g_s1 = bitsf(g[7]);
-    s.g_clock = bitsf(g[8]); s.g_shot = bitsf(g[9]); s.g_bask = bitsf(g[10]); s.g_oob = bitsf(g[11]);
-    s.g_inbclk = bitsf(g[12]); s.g_1v1 = (int32_t)g[13];
-    s.reset_now = c.world_clock[w];
-    s.rng_ctr = c.rng_counter[w];
-    const float *bp = c.ball_pos + w * 3, *bv = c.ball_vel + w * 3;
-    s.bx = bp[0]; s.by = bp[1]; s.bz = bp[2];
-    s.bvx = bv[0]; s.bvy = bv[1]; s.bvz = bv[2];
-    const int32_t *ph = c.ball_physics + w * 7;
-    s.fl = ph[0]; s.lta = ph[1]; s.ltt = ph[2]; s.sba = ph[3]; s.sbt = ph[4]; s.spv = ph[5]; s.gin = ph[6];
-    uint32_t gb[2];
-    load_words<2>(c.ball_grabbed, w, gb);
-    s.grab = (int32_t)gb[0]; s.holder = (int32_t)gb[1];
+    WorldRaw r;
+    r.load(p, w);
+    r.commit(s);
 }
 
 template <int N>
 BB_HD void load_world_agent(World<N> &s, const Params &p, int64_t w, int i)
 {
-    const Columns &c = p.c;
-    const int64_t r = w * N + i;
-    uint32_t a[6], pos[3], ps[3], q[4], v[3], ib[2], at[10];
-    load_words<6>(c.action, r, a);
-    load_words<3>(c.agent_pos, r, pos);
-    load_words<3>(c.possession, r, ps);
-    load_words<4>(c.orientation, r, q);
-    load_words<3>(c.agent_vel, r, v);
-    load_words<2>(c.inbounding, r, ib);
-    load_words<10>(c.attributes, r, at);
-    s.rst[i] = c.reset[r];
-#pragma unroll
-    for (int k = 0; k < 6; k++) s.act[i][k] = (int32_t)a[k];
-    s.px[i] = bitsf(pos[0]); s.py[i] = bitsf(pos[1]); s.pz[i] = bitsf(pos[2]);
-    s.has[i] = (int32_t)ps[0]; s.bid[i] = (int32_t)ps[1]; s.pw[i] = (int32_t)ps[2];
-    s.qw[i] = bitsf(q[0]); s.qx[i] = bitsf(q[1]); s.qy[i] = bitsf(q[2]); s.qz[i] = bitsf(q[3]);
-    s.vx[i] = bitsf(v[0]); s.vy[i] = bitsf(v[1]); s.vz[i] = bitsf(v[2]);
-    s.cd[i] = c.cooldown[r];
-    s.step[i] = c.cur_step[r];
-    s.inb[i] = (int32_t)ib[0]; s.allow[i] = (int32_t)ib[1];
-#pragma unroll
-    for (int k = 0; k < 10; k++) s.attr[i][k] = bitsf(at[k]);
-    const uint32_t *t = c.team + r * 5;
-    s.team[i] = (int32_t)t[0];
-    s.dhoop[i] = (int32_t)t[4];
-    s.rew[i] = 0.f; s.done[i] = 0.f;  // rewritten by tick before any read
-#pragma unroll
-    for (int k = 0; k < 4; k++) s.msk[i][k] = 0;  // rewritten by actionMaskSystem
+    AgentRaw<N> r;
+    r.load(p, w, i);
+    r.commit(s, i);
 }
 
 // Diagnostics A/B: BB_FULL_ROWS rewrites the whole GameState and Attributes

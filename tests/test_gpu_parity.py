@@ -113,6 +113,20 @@ def test_gpu_more_agents_equal_host_executor(n_agents):
         assert torch.equal(g._views[name].cpu(), h._views[name]), name
 
 
+@pytest.mark.parametrize("n_agents,W", [(4, 40000), (10, 24000)])
+def test_gpu_more_agents_many_waves(n_agents, W):
+    """More world groups than the GPU holds waves at once (several waves per
+    slot over the launch), a partial last group included (W is not a multiple
+    of the worlds per wave): device == host executor bit for bit."""
+    g = make_sim(ExecMode.CUDA, W, num_agents=n_agents, per_world_rng=True)
+    h = make_sim(ExecMode.CPU, W, num_agents=n_agents, per_world_rng=True)
+    g.step_n(120, random_actions=True)
+    h.step_n(120, random_actions=True)
+    torch.cuda.synchronize()
+    for name in g._views:
+        assert torch.equal(g._views[name].cpu(), h._views[name]), name
+
+
 @pytest.mark.parametrize("flags", [dict(tag_mask=False), dict(one_on_one=False), dict(tag_mask=False, one_on_one=False)])
 def test_gpu_game_variants(flags):
     """Grab/pass (tag override off) and full-game inbound paths."""
