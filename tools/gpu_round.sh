@@ -91,13 +91,15 @@ for s in $STEPS; do
                 --worlds $w --agents $n --steps 20 --warmup 5 --no-cpu-baseline --no-e2e ) || exit $?
         done
         python3 tools/traffic.py "$OUT/pmc_W${w}_N${n}_FETCH_SIZE" "$OUT/pmc_W${w}_N${n}_WRITE_SIZE" W${w}_N${n} \
-            --kernel "k_step<$n, 0>" --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
+            --kernel "k_step<$n, 0," --out "$OUT/traffic.json" | tee -a "$OUT/summary.txt"
         ;;
     profx:*) v=${s#profx:}; w=${v%%:*}; n=${v#*:}  # profx:<worlds>:<agents>: kernel stats of that bench line
         ( cd /tmp && export TMPDIR=/tmp && run "prof_W${w}_N${n}" 600 rocprofv3 --kernel-trace --stats \
             -d "$OUT/prof_W${w}_N${n}" -o run --output-format csv -- python3 "$ROOT/bench.py" \
             --worlds $w --agents $n --steps 200 --warmup 20 --no-cpu-baseline --no-e2e ) || exit $?
         ;;
+    benchrw:*) v=${s#benchrw:}; w=${v%%:*}; k=${v#*:}  # benchrw:<worlds>:<K>: rollouts of K steps
+        run "bench_W${w}_R$k" 600 python bench.py --worlds $w --rollout $k --steps $((32*k)) --warmup $k --no-cpu-baseline ;;
     benchx:*) v=${s#benchx:}; w=${v%%:*}; n=${v#*:}
         run "bench_W${w}_N${n}" 600 python bench.py --worlds $w --agents $n --steps 300 --warmup 30 --no-cpu-baseline ;;
     pmcv:*) v=${s#pmcv:}
