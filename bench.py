@@ -127,6 +127,9 @@ def main():
                     help="diagnostics: rollouts without recorded outputs (each step rewrites the sim's own tensors)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end leg (env.py's step through Python: slice write, step, 3 clones)")
+    ap.add_argument("--dist", action="store_true",
+                    help="start the process group (RCCL on the GPU) even at world size 1: exercises the "
+                         "multi-rank barrier / max-reduce path on one device")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
@@ -147,11 +150,14 @@ def main():
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    if world_size > 1:
+    use_dist = world_size > 1 or args.dist
+    if use_dist:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         if on_gpu:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world_size)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world_size)
 
     import madrona_basketball_amd as mba
     from madrona_basketball_amd import _lib
@@ -170,12 +176,12 @@ def main():
 
     def barrier():
         sync()
-        if world_size > 1:
+        if use_dist:
             dist.barrier()
         sync()
 
     def max_over_ranks(x: float) -> float:
-        if world_size == 1:
+        if not use_dist:
             return x
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -337,7 +343,7 @@ def main():
         out["cpu_baseline"] = cpu
         out["cpu_executor"] = cpu_exec
         print(json.dumps(out), flush=True)
-    if world_size > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

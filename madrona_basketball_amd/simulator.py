@@ -50,6 +50,14 @@ class Tensor:
 _TORCH_DTYPE = {_lib.DTYPE_INT32: torch.int32, _lib.DTYPE_FLOAT32: torch.float32}
 
 
+def _raw_stream(device_index: int) -> int:
+    """Torch's current HIP stream on the device, as a raw handle."""
+    get = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+    if get is not None:
+        return get(device_index)
+    return torch.cuda.current_stream(device_index).cuda_stream
+
+
 class SimpleGridworldSimulator:
     def __init__(self, discrete_x: int, discrete_y: int, start_x: float, start_y: float,
                  max_episode_length: int, exec_mode, num_worlds: int, gpu_id: int = -1,
@@ -100,6 +108,7 @@ class SimpleGridworldSimulator:
         _lib.check(L.bb_create_with_buffers(ctypes.byref(cfg), bufs, _lib.NUM_SLOTS, ctypes.byref(handle)),
                    "SimpleGridworldSimulator")
         self._h = handle
+        self._bb_step = L.bb_step
         self._views = {}
         for name, eid in _lib.EXPORT_IDS.items():
             ptr = ctypes.c_void_p()
@@ -127,13 +136,18 @@ class SimpleGridworldSimulator:
 
     def _stream(self):
         if self._device.type == "cuda":
-            return ctypes.c_void_p(torch.cuda.current_stream(self._device).cuda_stream)
+            return ctypes.c_void_p(_raw_stream(self._device.index))
         return ctypes.c_void_p(None)
 
     # ------------------------------------------------------------ reference API
     def step(self) -> None:
-        """Manager::step (src/mgr.cpp:243-246)."""
-        _lib.check(_lib.load().bb_step(self._h, self._stream()), "step")
+        """Manager::step (src/mgr.cpp:243-246).  The per-call Python work is one
+        ctypes call with torch's current raw stream (env.py calls this once per
+        environment step)."""
+        stream = _raw_stream(self._device.index) if self._device.type == "cuda" else None
+        rc = self._bb_step(self._h, stream)
+        if rc != _lib.OK:
+            _lib.check(rc, "step")
 
     def set_action(self, world_idx: int, agent_idx: int, move_speed: int, move_angle: int, rotate: int,
                    grab: int, pass_: int = None, shoot: int = None, **kw) -> None:
