@@ -1115,12 +1115,17 @@ static_assert(HALF_SHOULDER > 0.2144f && HALF_SHOULDER < 0.2146f && HALF_DEPTH >
               "COLLIDE_CULL assumes the 0.429 x 0.1 agent rectangle");
 
 template <int N>
-BB_HD void collide_pair(World<N> &s, int a, int b)
+BB_HD bool collide_near(const World<N> &s, int a, int b)
 {
-    {
-        const float dx = s.px[b] - s.px[a], dy = s.py[b] - s.py[a];
-        if (dx * dx + dy * dy > COLLIDE_CULL * COLLIDE_CULL) return;
-    }
+    const float dx = s.px[b] - s.px[a], dy = s.py[b] - s.py[a];
+    return !(dx * dx + dy * dy > COLLIDE_CULL * COLLIDE_CULL);
+}
+
+// Returns whether the pair collided (positions changed).
+template <int N>
+BB_HD bool collide_pair(World<N> &s, int a, int b)
+{
+    if (!collide_near(s, a, b)) return false;
     const F3 ca = s.pos(a), fa = forward(s.q(a));
     const F3 ra = f3(fa.y, -fa.x, 0.f);
     const F3 hwa = ra * HALF_SHOULDER, hda = fa * HALF_DEPTH;
@@ -1135,7 +1140,7 @@ BB_HD void collide_pair(World<N> &s, int a, int b)
 #pragma unroll
     for (int k = 0; k < 4; k++) {
         const Proj pa = project(va, axes[k]), pb = project(vb, axes[k]);
-        if (!(pa.mx > pb.mn && pb.mx > pa.mn)) return;  // separating axis
+        if (!(pa.mx > pb.mn && pb.mx > pa.mn)) return false;  // separating axis
         const float ov = minf(pa.mx, pb.mx) - maxf(pa.mn, pb.mn);
         if (ov < min_ov) { min_ov = ov; mtv = axes[k]; }
     }
@@ -1148,15 +1153,48 @@ BB_HD void collide_pair(World<N> &s, int a, int b)
     if (dot(cb - ca, corr) < 0.f) corr = -corr;
     s.set_pos(a, s.pos(a) - (corr * min_ov) * 0.5f);
     s.set_pos(b, s.pos(b) + (corr * min_ov) * 0.5f);
+    return true;
 }
 
-template <int N>
-BB_HD void sys_collisions(World<N> &s)
+// agentCollisionSystem over the pairs a < b in order.  With the world in
+// indexable memory (N >= LDS_WORLD_MIN_N) the cull tests of all pairs run
+// first, agent a's lane testing pairs (a, b > a) on the positions as they
+// are before any pair resolves; pairs are then visited in order through the
+// close ones only, until a pair collides: its agents moved, so from the next
+// pair on every pair is tested again on the current positions (the plain
+// serial loop).  Before the first collision no position has changed, so a
+// pair that was far then is far when its turn comes: the same pairs collide,
+// in the same order, as in the serial loop.
+template <int N, class A = EachAgent>
+BB_HD void sys_collisions(World<N> &s, const A &ag = A())
 {
+    if constexpr (N < LDS_WORLD_MIN_N) {
 #pragma unroll
-    for (int a = 0; a < N; a++)
+        for (int a = 0; a < N; a++)
 #pragma unroll
-        for (int b = a + 1; b < N; b++) collide_pair(s, a, b);
+            for (int b = a + 1; b < N; b++) collide_pair(s, a, b);
+    } else {
+        uint32_t near[N];  // bit b of near[a]: pair (a, b), b > a, within the cull distance
+        ag.all([&](int a) {
+            uint32_t m = 0;
+            for (int b = a + 1; b < N; b++)
+                if (collide_near(s, a, b)) m |= 1u << b;
+            return m;
+        }, near);
+        for (int a = 0; a < N; a++) {
+            uint32_t m = near[a];
+            while (m) {
+                const int b = __builtin_ctz(m);
+                m &= m - 1;
+                if (collide_pair(s, a, b)) {  // positions changed: the rest as the serial loop
+                    for (int b2 = b + 1; b2 < N; b2++) collide_pair(s, a, b2);
+                    for (int a2 = a + 1; a2 < N; a2++)
+                        for (int b2 = a2 + 1; b2 < N; b2++) collide_pair(s, a2, b2);
+                    return;
+                }
+            }
+        }
+    }
 }
 
 // ---- hardCodeDefenseSystem (game.cpp:651-755), one agent --------------
@@ -1663,7 +1701,7 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t s
     BB_RUN(14, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })  // resetSystem
     ag.mark(6);
     BB_RUN(15, sys_points_worth(s, c, ag))
-    BB_RUN(16, sys_collisions(s))
+    BB_RUN(16, sys_collisions(s, ag))
     BB_RUN(17, sys_defense(s, c, ag))
 #undef BB_RUN
 }

@@ -14,6 +14,7 @@ NAMES = {1: "tick", 2: "actionMask", 3: "moveAgent", 4: "grab", 5: "pass", 6: "s
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, default=65536)
+    ap.add_argument("--agents", type=int, default=2)
     ap.add_argument("--iters", type=int, default=100)
     ap.add_argument("--rounds", type=int, default=3)
     a = ap.parse_args()
@@ -23,7 +24,8 @@ def main():
     L = _lib.load()
     L.bb_diag_time.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
-    sim = mba.SimpleGridworldSimulator(32, 17, 15.7575, 8.382, 39600, mba.ExecMode.CUDA, a.worlds, 0, per_world_rng=True)
+    sim = mba.SimpleGridworldSimulator(32, 17, 15.7575, 8.382, 39600, mba.ExecMode.CUDA, a.worlds, 0,
+                                       num_agents=a.agents, per_world_rng=True)
     sim.step_n(50, random_actions=True)
     torch.cuda.synchronize()
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
