@@ -18,6 +18,7 @@
 // step (src/game.cpp:1467-1523, src/sim.cpp:99-124) with one launch.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <cstdlib>
 #include <type_traits>
 #include "bb_launch.h"
 #include "bb_sim.h"
@@ -29,6 +30,27 @@
 namespace bb {
 
 constexpr int WAVE = 64;
+
+// Cache policy of the observation-row stores (the bulk of a step's bytes):
+// -1 a plain global store; otherwise a buffer store with these aux bits
+// (gfx950: 1 sc0, 2 nt, 16 sc1 -- sc1 writes the line through and drops it
+// from the XCD's L2, so no dirty row lines are left for the end-of-kernel
+// write-back).
+#ifndef BB_STEP_AUX
+#define BB_STEP_AUX -1  // k_step, rows cache-resident
+#endif
+#ifndef BB_LINES_AUX
+#define BB_LINES_AUX 2  // k_step, state beyond the Infinity Cache
+#endif
+#ifndef BB_ROLLOUT_AUX
+#define BB_ROLLOUT_AUX 2  // k_rollout: rows into a fresh K-step buffer
+#endif
+#ifndef BB_SHARED_AUX
+#define BB_SHARED_AUX -1  // N >= 4, rows and columns while the step fits the cache
+#endif
+#ifndef BB_SHARED_BEYOND_AUX
+#define BB_SHARED_BEYOND_AUX 2  // N >= 4 beyond the cache
+#endif
 
 // The erf Taylor table (bb_math.h) copied to LDS by the workgroup's one
 // wave (k_rollout): shotPercentage's per-lane coefficient reads become LDS
@@ -89,8 +111,9 @@ struct Lanes {
 #endif
 // ALIGN: row writes end on this byte boundary (zero pieces added);
 // MAXP: at most this many 16-byte pieces of a row per pass.
-template <int N, int ALIGN = BB_OBS_WRITE_ALIGN, int MAXP = BB_OBS_PHASE_PIECES>
+template <int N, int ALIGN = BB_OBS_WRITE_ALIGN, int MAXP = BB_OBS_PHASE_PIECES, int STORE_AUX = BB_STEP_AUX>
 struct PhasedTile {
+    static constexpr int AUX = STORE_AUX;  // cache policy of the row stores (row_store)
     static constexpr int QU = (obs_used(N) + 3) / 4;  // pieces holding row values
     static constexpr int QA = (QU * 16 + ALIGN - 1) / ALIGN * ALIGN / 16;
     static constexpr int QW = QA < obs_width(N) / 4 ? QA : obs_width(N) / 4;  // pieces written
@@ -107,7 +130,7 @@ struct PhasedTile {
 // per step at 65 536 worlds).  k_step's 64 MiB rows stay cache-resident,
 // where the 416 written bytes of 2 x 13 pieces are cheaper.
 template <int N>
-using RolloutTile = PhasedTile<N, 128, 16>;
+using RolloutTile = PhasedTile<N, 128, 16, BB_ROLLOUT_AUX>;
 
 // k_step's tile.  LINES (state beyond the Infinity Cache): whole 128-byte
 // lines per pass, zero tail included, like k_rollout -- at 262 144 worlds
@@ -115,7 +138,7 @@ using RolloutTile = PhasedTile<N, 128, 16>;
 // otherwise 2 x 13 pieces (416 written bytes per row), cheaper while the rows
 // stay cache-resident (65 536 worlds: 21.95 vs 22.14 us).
 template <int N, bool LINES>
-using StepTile = typename std::conditional<LINES, RolloutTile<N>, PhasedTile<N>>::type;
+using StepTile = typename std::conditional<LINES, PhasedTile<N, 128, 16, BB_LINES_AUX>, PhasedTile<N>>::type;
 
 // RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
 // Indices are compile-time after unrolling, so the window test folds away and
@@ -247,8 +270,25 @@ struct LaneAgents {
 // world.  Pieces f = it*64 + lane: every LDS read of a batch is issued before
 // its stores, addresses are 32-bit offsets from the wave's first row.
 typedef float vf4 __attribute__((ext_vector_type(4)));  // plain 16-byte loads/stores
+typedef uint32_t vu4 __attribute__((ext_vector_type(4)));
 
-template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL, int QZ>
+template <int AUX>
+__device__ __forceinline__ void row_store(char *base, uint32_t off, vf4 v)
+{
+    if constexpr (AUX < 0) {
+        *(vf4 *)(base + off) = v;
+    } else {
+        // base is wave-uniform (the wave's first row): one descriptor per wave
+        const uint64_t b = (uint64_t)base;
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        char *ub = (char *)(((uint64_t)hi << 32) | lo);
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(ub, 0, 0x7fffffff, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(vu4, v), rs, (int)off, 0, AUX);
+    }
+}
+
+template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL, int QZ, int AUX>
 __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64_t staged, int lane)
 {
     // pieces q >= QZ of this pass are zeros (row padding), not read from the tile
@@ -277,16 +317,16 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
         }
 #pragma unroll
         for (int j = 0; j < BS; j++)
-            if (b0 + j < QT && ok[j]) *(vf4 *)(base + go[j]) = v[j];
+            if (b0 + j < QT && ok[j]) row_store<AUX>(base, go[j], v[j]);
     }
 }
 
-template <int N, int QT, int RS, int Q0, int QN, int RSTR, int QZ = QN>
+template <int N, int QT, int RS, int Q0, int QN, int RSTR, int QZ = QN, int AUX = -1>
 __device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane)
 {
     char *base = (char *)(obs + row0 * obs_width(N) + 4 * Q0);  // wave-uniform
-    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true, QZ>(tile, base, staged, lane);
-    else flush_rows<N, QT, RS, Q0, QN, RSTR, false, QZ>(tile, base, staged, lane);
+    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true, QZ, AUX>(tile, base, staged, lane);
+    else flush_rows<N, QT, RS, Q0, QN, RSTR, false, QZ, AUX>(tile, base, staged, lane);
 }
 
 struct Intrinsic {
@@ -313,7 +353,7 @@ __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, cons
     __syncthreads();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
     constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
-    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ>(tile, obs, row0, __ballot(fast), lane);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, row0, __ballot(fast), lane);
     if constexpr (PHASE + 1 < T::PH) {
         __syncthreads();
         obs_phases<N, MODE, T, PHASE + 1>(v, c, sh, share, fast, tile, obs, row0, lane, ib);
@@ -768,7 +808,7 @@ struct LaneSources {
 // per observer a (the row loop is unrolled over a), before the loop: per
 // piece the loop does 4 LDS reads and one store; the row's team (obs 0-22
 // entries) is a wave-uniform offset.
-template <int N>
+template <int N, int AUX>
 __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
@@ -786,7 +826,7 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
             dtm[p][c] = esw(piece_src<N>(code[c], 0, 1)) - esw(piece_src<N>(code[c], 0, 0));  // context entries only
         }
     }
-    char *base = (char *)(obs + row0 * obs_width(N)) + lane * 16;
+    char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
     for (int slot = 0; slot < WPW; slot++) {
         const float *e = sm.e[slot];
 #pragma unroll
@@ -799,7 +839,7 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
                 if (p * WAVE + lane < QR) {
                     const float v0 = e[src[p][a][0] + (dtm[p][0] & tmask)], v1 = e[src[p][a][1] + (dtm[p][1] & tmask)];
                     const float v2 = e[src[p][a][2] + (dtm[p][2] & tmask)], v3 = e[src[p][a][3] + (dtm[p][3] & tmask)];
-                    *(vf4 *)(base + ((uint32_t)r * QR + p * WAVE) * 16u) = vf4{v0, v1, v2, v3};
+                    row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, vf4{v0, v1, v2, v3});
                 }
             }
         }
@@ -834,9 +874,12 @@ struct SharedTiled {
     static constexpr bool value = BB_SHARED_TILE != 0;
 };
 
-template <int N, int MODE>
+// BEYOND: the step's bytes far exceed the Infinity Cache -- rows and columns
+// are stored non-temporally (see BB_SHARED_BEYOND_AUX).
+template <int N, int MODE, bool BEYOND = false>
 __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm)
 {
+    constexpr int AUX = BEYOND ? BB_SHARED_BEYOND_AUX : BB_SHARED_AUX;
     constexpr int WPW = SharedLds<N>::WPW, OW = obs_width(N);
     const int lane = threadIdx.x;
     // lanes past WPW*N mirror agents of the last world: they run its systems
@@ -888,11 +931,11 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();
     }
     if (active) {
-        store_world_agent(s, p, w * N + k, k, &lo.agent);
+        store_world_agent<N, AUX>(s, p, w * N + k, k, &lo.agent);
         if (k == 0) {
             Orig<N> o;
             set_world_orig(o, lo.world);
-            store_world_shared(s, p, w, &o);
+            store_world_shared<N, AUX>(s, p, w, &o);
         }
     }
     trace_point<MODE>(p, 8);
@@ -917,7 +960,7 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();  // the world state is dead: the source table overlays it
         if (active) src.put(sm.e[slot], k, share);
         __syncthreads();
-        emit_pieces<N>(sm, rows, p.c.obs, w0 * N, lane);
+        emit_pieces<N, AUX>(sm, rows, p.c.obs, w0 * N, lane);
         trace_point<MODE>(p, 9);
         return;
     }
@@ -1063,7 +1106,7 @@ __global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
             const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
             for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
         }
-        step_shared_world<N, MODE>(p, (float *)tile4, sm);
+        step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm);
     } else if constexpr (Lanes<N>::LPW == N) {
         step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);
     } else {
@@ -1084,11 +1127,24 @@ __global__ __launch_bounds__(256) void k_init(const Params p)
 // Whole-line observation passes once a step's state and rows no longer fit
 // comfortably in the 256 MiB Infinity Cache (see StepTile).
 constexpr int64_t LINES_MIN_BYTES = 192ll << 20;
+// N >= 4: the rows and columns are stored non-temporally once a step's bytes
+// exceed this (default 384 MiB; MADRONA_BB_NT_MIN_MB overrides it for A/B
+// timing).  Measured at 65 536 worlds: N = 4 (266 MB per step) 69.6 us plain
+// vs 73.9 nt; N = 10 (1.28 GB) 343 vs 323.
+inline int64_t shared_beyond_bytes()
+{
+    static const int64_t v = [] {
+        const char *e = getenv("MADRONA_BB_NT_MIN_MB");
+        return (int64_t)(e && *e ? atoll(e) : 384) << 20;
+    }();
+    return v;
+}
 template <int N>
 bool step_lines(int64_t num_worlds)
 {
     const int64_t per_world = (int64_t)N * (obs_width(N) * 4 + 240) + 160;  // rows + state columns
-    return Lanes<N>::LPW == N && !Lanes<N>::SHARED && num_worlds * per_world > LINES_MIN_BYTES;
+    if constexpr (Lanes<N>::SHARED) return num_worlds * per_world > shared_beyond_bytes();
+    return Lanes<N>::LPW == N && num_worlds * per_world > LINES_MIN_BYTES;
 }
 
 template <int N>

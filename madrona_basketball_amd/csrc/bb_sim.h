@@ -322,11 +322,43 @@ BB_HD void load_words(const void *base, int64_t w, uint32_t (&o)[NW])
 #endif
 }
 
-template <int NW>
+// AUX: cache-policy bits of the device stores (-1: plain global stores;
+// otherwise buffer stores with these aux bits -- gfx950: 2 nt, 16 sc1; `base`
+// must then be wave-uniform, the column's own base).
+template <int NW, int AUX = -1>
 BB_HD void store_words(void *base, int64_t w, const uint32_t (&o)[NW])
 {
     uint32_t *p = (uint32_t *)base + w * NW;
 #if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (AUX >= 0) {
+        // descriptor at the first active lane's chunk (wave-uniform); the
+        // other lanes' chunks follow it (w grows with the lane), so the
+        // 32-bit offsets stay small at any column size
+        const uint64_t wu = (uint64_t)w;
+        const int64_t wf = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wu >> 32)) << 32) |
+                                     __builtin_amdgcn_readfirstlane((uint32_t)wu));
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc((uint32_t *)base + wf * NW, 0, 0x7fffffff, 0x00020000);
+        const int off = (int)((w - wf) * NW * 4);
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        if constexpr (NW % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < NW / 4; k++)
+                __builtin_amdgcn_raw_buffer_store_b128(u4{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, rs,
+                                                       off + 16 * k, 0, AUX);
+        } else if constexpr (NW % 2 == 0) {
+#pragma unroll
+            for (int k = 0; k < NW / 2; k++)
+                __builtin_amdgcn_raw_buffer_store_b64(u2{o[2 * k], o[2 * k + 1]}, rs, off + 8 * k, 0, AUX);
+        } else if constexpr (NW == 3) {
+            __builtin_amdgcn_raw_buffer_store_b96(u3{o[0], o[1], o[2]}, rs, off, 0, AUX);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NW; k++) __builtin_amdgcn_raw_buffer_store_b32(o[k], rs, off + 4 * k, 0, AUX);
+        }
+        return;
+    }
     if constexpr (NW % 4 == 0) {
 #pragma unroll
         for (int k = 0; k < NW / 4; k++)
@@ -2000,7 +2032,7 @@ BB_HD void load_world_agent(World<N> &s, const Params &p, int64_t w, int i)
 
 // World-level columns (GameState, WorldClock, RNG counter, ball).  With `o`,
 // the event-only words are rewritten only when changed (see Orig).
-template <int N>
+template <int N, int CA = -1>
 BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, const Orig<N> *o = nullptr)
 {
     const Columns &c = p.c;
@@ -2013,10 +2045,10 @@ BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, con
             if (k != 8 && k != 9) game_ev |= g[k] != o->game[k];
     }
     if (game_ev) {
-        store_words<14>(c.game_state, w, g);
+        store_words<14, CA>(c.game_state, w, g);
     } else {  // game and shot clock only
         const uint32_t clk[2] = {g[8], g[9]};
-        store_words<2>(c.game_state + w * 14 + 8, 0, clk);
+        store_words<2, CA>(c.game_state + 8, w * 7, clk);  // words 14w+8, 14w+9
     }
     if (!o || (uint32_t)s.reset_now != o->clock) c.world_clock[w] = s.reset_now;
     if (!o || s.rng_ctr != o->rng) c.rng_counter[w] = s.rng_ctr;
@@ -2031,14 +2063,14 @@ BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, con
         for (int k = 0; k < 7; k++) d[k] = ph[k];
     }
     const uint32_t gb[2] = {(uint32_t)s.grab, (uint32_t)s.holder};
-    if (!o || differ(gb, o->grab)) store_words<2>(c.ball_grabbed, w, gb);
+    if (!o || differ(gb, o->grab)) store_words<2, CA>(c.ball_grabbed, w, gb);
 }
 
 // Per-agent columns of agent i (row w*N + i of every [W][N][...] column).
 // Team changes only inside generate/reset, which write it directly.  With
 // `o` (agent i's event-only words as loaded) those are rewritten only when
 // changed.
-template <int N>
+template <int N, int CA = -1>
 BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int i, const OrigAgent *o = nullptr)
 {
     const Columns &c = p.c;
@@ -2055,17 +2087,17 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
 #pragma unroll
     for (int k = 0; k < 10; k++) at[k] = fbits(s.attr[i][k]);
     if (!o || s.rst[i] != o->rst) c.reset[r] = s.rst[i];
-    store_words<6>(c.action, r, a);
-    store_words<4>(c.action_mask, r, m);
-    store_words<3>(c.agent_pos, r, pos);
+    store_words<6, CA>(c.action, r, a);
+    store_words<4, CA>(c.action_mask, r, m);
+    store_words<3, CA>(c.agent_pos, r, pos);
     c.reward[r] = s.rew[i];
     c.done[r] = s.done[i];
-    store_words<3>(c.possession, r, ps);
-    store_words<4>(c.orientation, r, q);
-    store_words<3>(c.agent_vel, r, v);
+    store_words<3, CA>(c.possession, r, ps);
+    store_words<4, CA>(c.orientation, r, q);
+    store_words<3, CA>(c.agent_vel, r, v);
     c.cooldown[r] = s.cd[i];
     c.cur_step[r] = s.step[i];
-    if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2>(c.inbounding, r, ib);
+    if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2, CA>(c.inbounding, r, ib);
     bool attr_ev = o == nullptr || BB_FULL_ROWS;
     if (o) {
 #pragma unroll
@@ -2073,7 +2105,7 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
         attr_ev |= at[9] != o->attr[5];
     }
     if (attr_ev) {
-        store_words<10>(c.attributes, r, at);
+        store_words<10, CA>(c.attributes, r, at);
     } else {  // target position (5-7) and shot percentage (8)
         uint32_t *d = (uint32_t *)c.attributes + r * 10 + 5;
 #pragma unroll
