@@ -49,7 +49,10 @@ constexpr int WAVE = 64;
 #define BB_SHARED_AUX -1  // N >= 4, rows and columns while the step fits the cache
 #endif
 #ifndef BB_SHARED_BEYOND_AUX
-#define BB_SHARED_BEYOND_AUX 2  // N >= 4 beyond the cache
+#define BB_SHARED_BEYOND_AUX 2  // N >= 4 beyond the cache: rows
+#endif
+#ifndef BB_SHARED_BEYOND_COL_AUX
+#define BB_SHARED_BEYOND_COL_AUX 2  // N >= 4 beyond the cache: state columns
 #endif
 
 // The erf Taylor table (bb_math.h) copied to LDS by the workgroup's one
@@ -880,6 +883,7 @@ template <int N, int MODE, bool BEYOND = false>
 __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm)
 {
     constexpr int AUX = BEYOND ? BB_SHARED_BEYOND_AUX : BB_SHARED_AUX;
+    constexpr int CAUX = BEYOND ? BB_SHARED_BEYOND_COL_AUX : BB_SHARED_AUX;
     constexpr int WPW = SharedLds<N>::WPW, OW = obs_width(N);
     const int lane = threadIdx.x;
     // lanes past WPW*N mirror agents of the last world: they run its systems
@@ -931,11 +935,11 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();
     }
     if (active) {
-        store_world_agent<N, AUX>(s, p, w * N + k, k, &lo.agent);
+        store_world_agent<N, CAUX>(s, p, w * N + k, k, &lo.agent);
         if (k == 0) {
             Orig<N> o;
             set_world_orig(o, lo.world);
-            store_world_shared<N, AUX>(s, p, w, &o);
+            store_world_shared<N, CAUX>(s, p, w, &o);
         }
     }
     trace_point<MODE>(p, 8);
