@@ -85,17 +85,30 @@ void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *d
 }
 
 // Coalesced streaming probe: item i reads read_q float4 and writes write_q
-// float4, laid out [q][item] so every wave instruction is 1 KiB contiguous.
-__global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q)
+// float4.  pattern 0 lays them out [q][item] (the waves resident at once
+// sweep one contiguous window); pattern 1 gives each wave a region of its own
+// that it reads/writes front to back (as k_step's rows: 64 pieces of one
+// region per instruction).  Every wave instruction is 1 KiB contiguous; nt:
+// non-temporal stores.
+__global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q,
+                                                     int write_q, int pattern, int nt)
 {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= items) return;
+    const int64_t wave = i >> 6, lane = i & 63;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int q = 0; q < read_q; q++) {
-        const float4 v = src[(int64_t)q * items + i];
+        const int64_t at = pattern ? (wave * read_q + q) * 64 + lane : (int64_t)q * items + i;
+        const float4 v = src[at];
         acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    for (int q = 0; q < write_q; q++) dst[(int64_t)q * items + i] = acc;
+    for (int q = 0; q < write_q; q++) {
+        const int64_t at = pattern ? (wave * write_q + q) * 64 + lane : (int64_t)q * items + i;
+        typedef float v4 __attribute__((ext_vector_type(4)));
+        const v4 a = {acc.x, acc.y, acc.z, acc.w};
+        if (nt) __builtin_nontemporal_store(a, (v4 *)&dst[at]);
+        else *(v4 *)&dst[at] = a;
+    }
 }
 
 static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
@@ -127,9 +140,11 @@ hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uin
     return hipGetLastError();
 }
 
-hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, hipStream_t s)
+hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, int pattern,
+                               int nt, hipStream_t s)
 {
-    hipLaunchKernelGGL(k_stream_probe, grid_for(items, 256), dim3(256), 0, s, src, dst, items, read_q, write_q);
+    hipLaunchKernelGGL(k_stream_probe, grid_for(items, 256), dim3(256), 0, s, src, dst, items, read_q, write_q, pattern,
+                       nt);
     return hipGetLastError();
 }
 

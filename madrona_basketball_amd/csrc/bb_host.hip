@@ -777,7 +777,8 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
     hipStream_t st = (hipStream_t)stream;
     float4 *src = nullptr, *dst = nullptr;
     const int64_t W = s->cfg.num_worlds;
-    if (mode == 100) {
+    const bool probe = mode >= 100 && mode <= 103;  // 100 + 2*nt + region pattern
+    if (probe) {
         if (hipMalloc(&src, (size_t)W * read_q * 16) != hipSuccess || hipMalloc(&dst, (size_t)W * write_q * 16) != hipSuccess)
             return fail(BB_ERR_OOM, "probe buffers");
         (void)hipMemsetAsync(src, 0, (size_t)W * read_q * 16, st);
@@ -790,7 +791,7 @@ int bb_diag_time(bb_sim *s, int32_t mode, int32_t iters, int32_t read_q, int32_t
     pp.diag_dup = dup;
     pp.diag_keep = 0;
     auto once = [&]() -> hipError_t {
-        if (mode == 100) return bb::launch_stream_probe(src, dst, W, read_q, write_q, st);
+        if (probe) return bb::launch_stream_probe(src, dst, W, read_q, write_q, (mode - 100) & 1, (mode - 100) >> 1, st);
         return bb::launch_step(s->n, pp, st, mode);
     };
     hipError_t e = once();  // warm

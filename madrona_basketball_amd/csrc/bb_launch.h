@@ -75,7 +75,8 @@ void host_policy(const PolicyArgs &a);
 hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s);
 void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)
-hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, hipStream_t s);
+hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, int pattern,
+                               int nt, hipStream_t s);
 
 // Host executor (ExecMode.CPU): the same step code over a thread pool.
 int host_step(int n, const Params &p, int threads);

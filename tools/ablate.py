@@ -16,7 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 MODES = {0: "full (LDS-staged obs)", 1: "io only", 2: "io + obs rows", 3: "full (lane-strided obs, v1)",
-         4: "full minus obs", 100: "stream probe (same bytes, coalesced)"}
+         4: "full minus obs", 100: "stream probe (same bytes, coalesced)",
+         101: "stream probe, per-wave regions", 102: "stream probe, nt stores",
+         103: "stream probe, per-wave regions, nt"}
 
 
 def main():
@@ -46,7 +48,7 @@ def main():
     read_q, write_q = (reads + 15) // 16, (B - reads + 15) // 16
     # algorithmic bytes each mode moves per world: the variants without the
     # observation pass do not write the rows, the probe moves its own pieces
-    moved = {0: B, 1: B - obs_b, 2: B, 3: B, 4: B - obs_b, 100: 16 * (read_q + write_q)}
+    moved = {0: B, 1: B - obs_b, 2: B, 3: B, 4: B - obs_b, **{m: 16 * (read_q + write_q) for m in (100, 101, 102, 103)}}
     modes = {m: MODES[m] for m in (args.only if args.only is not None else MODES)}
     res = {m: [] for m in modes}
     stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
