@@ -48,6 +48,15 @@ constexpr int WAVE = 64;
 #ifndef BB_SHARED_AUX
 #define BB_SHARED_AUX -1  // N >= 4, rows and columns while the step fits the cache
 #endif
+// Wave priority (s_setprio) while a wave of the shared-world kernel emits its
+// rows / issues its state loads: memory work of one wave ahead of the
+// systems of the others on its SIMD.
+#ifndef BB_PRIO_ROWS
+#define BB_PRIO_ROWS 0
+#endif
+#ifndef BB_PRIO_LOAD
+#define BB_PRIO_LOAD 0
+#endif
 #ifndef BB_SHARED_BEYOND_AUX
 #define BB_SHARED_BEYOND_AUX 2  // N >= 4 beyond the cache: rows
 #endif
@@ -901,6 +910,7 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     trace_point<MODE>(p, 0);
     constexpr bool PIECES = BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value;
 
+    if constexpr (BB_PRIO_LOAD > 0) __builtin_amdgcn_s_setprio(BB_PRIO_LOAD);
     if (active) {
         // every load issued before the first LDS write (one memory latency)
         AgentRaw<N> ar;
@@ -911,6 +921,7 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         if (k == 0) wr.commit(s);
     }
     __syncthreads();
+    if constexpr (BB_PRIO_LOAD > 0) __builtin_amdgcn_s_setprio(0);
     // event-only words as loaded (store only on change, see Orig)
     LaneOrig lo;
     if (active) {
@@ -964,6 +975,8 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
         __syncthreads();  // the world state is dead: the source table overlays it
         if (active) src.put(sm.e[slot], k, share);
         __syncthreads();
+        // the row pass (memory-bound) ahead of other waves' systems (VALU)
+        if constexpr (BB_PRIO_ROWS > 0) __builtin_amdgcn_s_setprio(BB_PRIO_ROWS);
         emit_pieces<N, AUX>(sm, rows, p.c.obs, w0 * N, lane);
         trace_point<MODE>(p, 9);
         return;
