@@ -113,11 +113,14 @@ def test_gpu_more_agents_equal_host_executor(n_agents):
         assert torch.equal(g._views[name].cpu(), h._views[name]), name
 
 
-@pytest.mark.parametrize("n_agents,W", [(4, 40000), (10, 24000)])
+@pytest.mark.parametrize("n_agents,W", [(2, 140001), (4, 40000), (4, 110001), (6, 52003), (8, 32003), (10, 24000)])
 def test_gpu_more_agents_many_waves(n_agents, W):
     """More world groups than the GPU holds waves at once (several waves per
     slot over the launch), a partial last group included (W is not a multiple
-    of the worlds per wave): device == host executor bit for bit."""
+    of the worlds per wave): device == host executor bit for bit.  The sizes
+    past the Infinity Cache take the non-temporal store paths (N = 2 whole-line
+    rows above 192 MiB of state; N >= 4 rows and columns above 384 MiB per
+    step: 4 x 110001, 6 x 52003, 8 x 32003, 10 x 24000)."""
     g = make_sim(ExecMode.CUDA, W, num_agents=n_agents, per_world_rng=True)
     h = make_sim(ExecMode.CPU, W, num_agents=n_agents, per_world_rng=True)
     g.step_n(120, random_actions=True)
