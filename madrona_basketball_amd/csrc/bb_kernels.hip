@@ -730,13 +730,24 @@ __device__ __forceinline__ int piece_src(uint32_t code, int a, int tm)
            + (int)((code >> 22) & 0x1Fu) * tm;
 }
 
+// N = 4: a world's agents are the 4 lanes of a DPP quad, so the per-agent
+// results are exchanged by quad_perm moves (LaneAgents) instead of through an
+// LDS buffer: 3.3 KB less LDS per wave, 12 waves per CU instead of 9.
+#ifndef BB_DPP_AGENTS
+#define BB_DPP_AGENTS 1
+#endif
+template <int N>
+struct DppAgents {
+    static constexpr bool value = BB_DPP_AGENTS && N == 4 && XW < INTRINSIC;
+};
+
 template <int N>
 struct SharedLds {
     static constexpr int WPW = WAVE / N;  // worlds per wave
     union {
         struct {
             World<N> world[WPW];
-            uint32_t x[WAVE][XW];              // systems: per-agent exchange
+            uint32_t x[DppAgents<N>::value ? 1 : WAVE][XW];  // systems: per-agent exchange
         };
         float e[WPW][ObsSrc<N>::ES];           // observation pass: row sources
     };
@@ -905,7 +916,10 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     const bool world_ok = w < p.num_worlds;  // uniform over the world's lanes
     const bool active = lane_used && world_ok;
     World<N> &s = sm.world[slot];
-    const LdsAgents<N, MODE> ag{k, slot, sm.x, &p};
+    using AG = typename std::conditional<DppAgents<N>::value, LaneAgents<N, MODE>, LdsAgents<N, MODE>>::type;
+    AG ag;
+    if constexpr (DppAgents<N>::value) ag = LaneAgents<N, MODE>{k, &p};
+    else ag = LdsAgents<N, MODE>{k, slot, sm.x, &p};
     Ctx c = make_ctx(p, w, active && k == 0);
     trace_point<MODE>(p, 0);
     constexpr bool PIECES = BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value;
