@@ -141,8 +141,14 @@ struct PhasedTile {
 // partial by a pass reach memory as partial writes (measured: 25.7 -> 18.1 us
 // per step at 65 536 worlds).  k_step's 64 MiB rows stay cache-resident,
 // where the 416 written bytes of 2 x 13 pieces are cheaper.
+#ifndef BB_LINES_ALIGN
+#define BB_LINES_ALIGN 128  // beyond-cache row writes end on this byte boundary
+#endif
+#ifndef BB_LINES_MAXP
+#define BB_LINES_MAXP 16
+#endif
 template <int N>
-using RolloutTile = PhasedTile<N, 128, 16, BB_ROLLOUT_AUX>;
+using RolloutTile = PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_ROLLOUT_AUX>;
 
 // k_step's tile.  LINES (state beyond the Infinity Cache): whole 128-byte
 // lines per pass, zero tail included, like k_rollout -- at 262 144 worlds
@@ -150,7 +156,7 @@ using RolloutTile = PhasedTile<N, 128, 16, BB_ROLLOUT_AUX>;
 // otherwise 2 x 13 pieces (416 written bytes per row), cheaper while the rows
 // stay cache-resident (65 536 worlds: 21.95 vs 22.14 us).
 template <int N, bool LINES>
-using StepTile = typename std::conditional<LINES, PhasedTile<N, 128, 16, BB_LINES_AUX>, PhasedTile<N>>::type;
+using StepTile = typename std::conditional<LINES, PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_LINES_AUX>, PhasedTile<N>>::type;
 
 // RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
 // Indices are compile-time after unrolling, so the window test folds away and

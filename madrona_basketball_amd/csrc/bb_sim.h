@@ -2024,10 +2024,13 @@ BB_HD void load_world_agent(World<N> &s, const Params &p, int64_t w, int i)
     r.commit(s, i);
 }
 
-// Diagnostics A/B: BB_FULL_ROWS rewrites the whole GameState and Attributes
-// rows every step (whole 64-byte segments) instead of only their changed words.
+// BB_FULL_ROWS: the whole GameState and Attributes rows are rewritten every
+// step instead of only their changed words (game/shot clock, Attributes 5-8),
+// so a wave's stores cover whole lines of those columns.  A/B (two repeats,
+// profiles/r02/o_full_rows_ab.txt): 65 536 x 2 21.85 -> 21.69 us, 262 144 x 2
+// 75.5 -> 75.2, N = 4 70.7 -> 69.5, N = 10 323.4 -> 320.6.
 #ifndef BB_FULL_ROWS
-#define BB_FULL_ROWS 0
+#define BB_FULL_ROWS 1
 #endif
 
 // World-level columns (GameState, WorldClock, RNG counter, ball).  With `o`,
