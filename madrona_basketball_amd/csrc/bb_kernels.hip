@@ -269,7 +269,10 @@ __device__ __forceinline__ void trace_resets(const Params &p, bool active, const
 // Agent policy of the agent-lane kernel (see EachAgent in bb_sim.h).  Called
 // at the top level of step_world_pre_obs, where the N lanes of a world are
 // converged.
-template <int G, int MODE>
+// OWN_APPLY: the world lives in LDS shared by its G lanes (the N = 4
+// shared-world kernel), so in each() a lane applies only its own agent's
+// result; with the world in every lane's registers each lane applies all G.
+template <int G, int MODE, bool OWN_APPLY = false>
 struct LaneAgents {
     int k;
     const Params *p;
@@ -278,6 +281,19 @@ struct LaneAgents {
     {
         static_assert(N == G, "one lane per agent");
         lane_gather<G>(f(k), out);
+    }
+    template <int N, class F, class P>
+    __device__ void each(F f, P apply) const
+    {
+        static_assert(N == G, "one lane per agent");
+        if constexpr (OWN_APPLY) {
+            apply(k, f(k));
+        } else {
+            decltype(f(0)) out[G];
+            lane_gather<G>(f(k), out);
+#pragma unroll
+            for (int i = 0; i < G; i++) apply(i, out[i]);
+        }
     }
     __device__ void mark(int point) const { trace_point<MODE>(*p, point); }
 };
@@ -655,6 +671,17 @@ struct LdsAgents {
 #pragma unroll
         for (int j = 0; j < N; j++) __builtin_memcpy(&out[j], x[slot * N + j], sizeof(T));
     }
+    // The world is in LDS: each lane applies its own agent's result (no
+    // exchange; agent i's f reads nothing another agent's apply writes, and
+    // the wave's reads all precede its writes in program order).  Lanes past
+    // the last world mirror its agents and write the same values.
+    template <int NN, class F, class P>
+    __device__ void each(F f, P apply) const
+    {
+        static_assert(NN == N, "one lane per agent");
+        apply(k, f(k));
+        __syncthreads();
+    }
     __device__ void mark(int point) const { trace_point<MODE>(*p, point); }
 };
 
@@ -922,9 +949,9 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     const bool world_ok = w < p.num_worlds;  // uniform over the world's lanes
     const bool active = lane_used && world_ok;
     World<N> &s = sm.world[slot];
-    using AG = typename std::conditional<DppAgents<N>::value, LaneAgents<N, MODE>, LdsAgents<N, MODE>>::type;
+    using AG = typename std::conditional<DppAgents<N>::value, LaneAgents<N, MODE, true>, LdsAgents<N, MODE>>::type;
     AG ag;
-    if constexpr (DppAgents<N>::value) ag = LaneAgents<N, MODE>{k, &p};
+    if constexpr (DppAgents<N>::value) ag = LaneAgents<N, MODE, true>{k, &p};
     else ag = LdsAgents<N, MODE>{k, slot, sm.x, &p};
     Ctx c = make_ctx(p, w, active && k == 0);
     trace_point<MODE>(p, 0);

@@ -235,6 +235,18 @@ struct EachAgent {
 #pragma unroll
         for (int i = 0; i < N; i++) out[i] = f(i);
     }
+    // Per-agent system whose agent i reads nothing another agent's apply
+    // writes: every f(i) from the state before the system, then apply(i, .)
+    // in creation order.  (A kernel whose lanes share the world in LDS lets
+    // each lane apply only its own agent's result, see bb_kernels.hip.)
+    template <int N, class F, class P>
+    BB_HD void each(F f, P apply) const
+    {
+        decltype(f(0)) out[N];
+        all(f, out);
+#pragma unroll
+        for (int i = 0; i < N; i++) apply(i, out[i]);
+    }
     BB_HD void mark(int) const {}
 };
 
@@ -783,10 +795,9 @@ BB_HD void apply_move(World<N> &s, int j, const MoveOut &o)
 template <int N, class A>
 BB_HD void sys_move_agents(World<N> &s, const Ctx &c, const A &ag)
 {
-    MoveOut o[N];  // agent i reads only its own columns
-    ag.all([&](int i) { return move_one(gather_move(s, i), *c.p); }, o);
-#pragma unroll
-    for (int i = 0; i < N; i++) apply_move(s, i, o[i]);
+    // agent i reads only its own columns
+    ag.template each<N>([&](int i) { return move_one(gather_move(s, i), *c.p); },
+                        [&](int i, const MoveOut &o) { apply_move(s, i, o); });
 }
 
 template <int N>
@@ -941,15 +952,14 @@ BB_HD void apply_shoot(World<N> &s, int i, const ShootOut &o)
 template <int N, class A>
 BB_HD void sys_shoot(World<N> &s, const Ctx &c, const A &ag)
 {
-    ShootOut o[N];
-    ag.all([&](int i) { return shoot_one(s, c, i); }, o);
+    // the stream position after every agent's draws, from the state before
+    // the system (apply_shoot changes nothing shoot_draws or shoot_one reads
+    // for another agent: only the holder's shot touches ball and possession)
     uint32_t draws = 0;
 #pragma unroll
-    for (int i = 0; i < N; i++) {
-        draws += shoot_draws(s, i);  // before apply_shoot changes what it reads
-    }
-#pragma unroll
-    for (int i = 0; i < N; i++) apply_shoot(s, i, o[i]);
+    for (int i = 0; i < N; i++) draws += shoot_draws(s, i);
+    ag.template each<N>([&](int i) { return shoot_one(s, c, i); },
+                        [&](int i, const ShootOut &o) { apply_shoot(s, i, o); });
     s.rng_ctr += draws;
 }
 
@@ -996,10 +1006,8 @@ BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
 template <int N, class A>
 BB_HD void sys_shot_percentage(World<N> &s, const Ctx &c, const A &ag)
 {
-    float v[N];  // reads nothing it writes
-    ag.all([&](int i) { return shot_pct_one(s, c, i); }, v);
-#pragma unroll
-    for (int i = 0; i < N; i++) s.attr[i][8] = v[i];
+    // reads nothing it writes
+    ag.template each<N>([&](int i) { return shot_pct_one(s, c, i); }, [&](int i, float v) { s.attr[i][8] = v; });
 }
 
 template <int N>
@@ -1119,10 +1127,8 @@ BB_HD int32_t points_worth_one(const World<N> &s, const Ctx &c, int i)
 template <int N, class A>
 BB_HD void sys_points_worth(World<N> &s, const Ctx &c, const A &ag)
 {
-    int32_t v[N];  // reads only pos/dhoop
-    ag.all([&](int i) { return points_worth_one(s, c, i); }, v);
-#pragma unroll
-    for (int i = 0; i < N; i++) s.pw[i] = v[i];
+    // reads only pos/dhoop
+    ag.template each<N>([&](int i) { return points_worth_one(s, c, i); }, [&](int i, int32_t v) { s.pw[i] = v; });
 }
 
 struct Proj { float mn, mx; };
@@ -1306,10 +1312,9 @@ BB_HD void apply_defense(World<N> &s, int j, const DefOut &o)
 template <int N, class A>
 BB_HD void sys_defense(World<N> &s, const Ctx &c, const A &ag)
 {
-    DefOut o[N];  // agent i reads only fields no other agent's defence writes
-    ag.all([&](int i) { return defense_one(s, c, i); }, o);
-#pragma unroll
-    for (int i = 0; i < N; i++) apply_defense(s, i, o[i]);
+    // agent i reads only fields no other agent's defence writes
+    ag.template each<N>([&](int i) { return defense_one(s, c, i); },
+                        [&](int i, const DefOut &o) { apply_defense(s, i, o); });
 }
 
 // ---- rewardSystem (game.cpp:811-870), one agent ------------------------
