@@ -1158,8 +1158,11 @@ __device__ __forceinline__ void start_skew()
     }
 }
 
+#ifndef BB_STEP_MINW
+#define BB_STEP_MINW 2  // waves per SIMD the register budget is sized for
+#endif
 template <int N, int MODE, bool LINES = false>
-__global__ __launch_bounds__(WAVE, 2) void k_step(const Params p)
+__global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
 {
     __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
     start_skew();

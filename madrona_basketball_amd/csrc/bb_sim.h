@@ -202,7 +202,10 @@ BB_HD constexpr int view_slot(int i, int k)
 
 // From this agent count on the GPU kernel keeps the world in LDS
 // (bb_kernels.hip, Lanes::SHARED), where an indexed access is one LDS load.
-constexpr int LDS_WORLD_MIN_N = 4;
+#ifndef BB_LDS_WORLD_MIN_N
+#define BB_LDS_WORLD_MIN_N 4
+#endif
+constexpr int LDS_WORLD_MIN_N = BB_LDS_WORLD_MIN_N;
 
 // Value of f(j) for j == i.  For register-resident worlds (N < 4) it is built
 // from selects: i may be a runtime value -- e.g. the lane's agent -- while
