@@ -510,6 +510,74 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 9);
 }
 
+// Timing experiment (diagnostic build, BB_STEP_BLOCKS > 1): each wave steps
+// B world blocks in turn, the next block's state loads issued ahead of this
+// block's systems and retired before its stores (the k_rollout discipline),
+// so a block's row stores drain under the next block's systems.  Same
+// results as k_step with one block per wave (every world is stepped once,
+// by the same code).
+#ifndef BB_STEP_BLOCKS
+#define BB_STEP_BLOCKS 1
+#endif
+template <int N, bool LINES, int B>
+__device__ __forceinline__ void step_agent_lanes_pipelined(const Params &p, float *tile)
+{
+    using T = StepTile<N, LINES>;
+    const int lane = threadIdx.x;
+    const int k = lane % N;
+    const int64_t nblk = (p.num_worlds + WAVE / N - 1) / (WAVE / N);
+    const int64_t stride = (int64_t)gridDim.x * (WAVE / N);
+    World<N> nxt;
+    {
+        const int64_t w = (int64_t)blockIdx.x * (WAVE / N) + lane / N;
+        if (w < p.num_worlds) load_world(nxt, p, w);
+    }
+    for (int b = 0; b < B; b++) {
+        const int64_t blk = (int64_t)blockIdx.x + (int64_t)b * gridDim.x;
+        if (blk >= nblk) break;  // uniform over the wave
+        const int64_t w0 = blk * (WAVE / N);
+        const int64_t w = w0 + lane / N;
+        const bool active = w < p.num_worlds;
+        const int64_t wn = w + stride;
+        const bool next_ok = b + 1 < B && wn < p.num_worlds;
+        const LaneAgents<N, MODE_FULL> ag{k, &p};
+        World<N> s = nxt;
+        World<N> v;
+        Ctx c = make_ctx(p, w, k == 0);
+        LaneOrig *lo = (LaneOrig *)(tile + lane * T::RS);
+        if (active) {
+            {
+                Orig<N> o;
+                capture(o, s);
+                LaneOrig x;
+                x.world = world_orig(o);
+                x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
+                *lo = x;
+            }
+            if (next_ok) load_world(nxt, p, wn);
+            step_world_pre_obs(s, c, ag);
+        }
+        // the prefetch retired here: what it waits for besides it are the
+        // previous block's stores, drained during these systems
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if (active) {
+            agent_view(s, v, k);
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            const LaneOrig x = *lo;
+            store_world_agent(v, p, w * N + k, 0, &x.agent);
+            if (k == 0) {
+                Orig<N> o;
+                set_world_orig(o, x.world);
+                store_world_shared(s, p, w, &o);
+            }
+        }
+        const int32_t ib = active ? inbounder_id(s) : -1;
+        const bool share = active && obs_sharable(s);
+        agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+        __syncthreads();  // the tile's rows (and parked words) are rewritten by the next block
+    }
+}
+
 // ------------------------------------------------------------------ rollout
 // K steps in one launch (agent lanes, N = 2): the world stays in registers
 // from the first load to the last store, so a step moves only its action
@@ -1174,6 +1242,8 @@ __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
             for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
         }
         step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm);
+    } else if constexpr (Lanes<N>::LPW == N && MODE == MODE_FULL && BB_STEP_BLOCKS > 1) {
+        step_agent_lanes_pipelined<N, LINES, BB_STEP_BLOCKS>(p, (float *)tile4);
     } else if constexpr (Lanes<N>::LPW == N) {
         step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);
     } else {
@@ -1219,11 +1289,14 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 {
     constexpr int WPB = Lanes<N>::WPB;
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+    // BB_STEP_BLOCKS world blocks per wave (the pipelined timing experiment)
+    constexpr int FB = (Lanes<N>::LPW == N && !Lanes<N>::SHARED) ? BB_STEP_BLOCKS : 1;
+    const dim3 grid_full((grid.x + FB - 1) / FB);
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
     case MODE_FULL:
-        if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid, block, 0, s, ev0, ev1, 0, p);
-        else BB_LAUNCH(MODE_FULL);
+        if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid_full, block, 0, s, ev0, ev1, 0, p);
+        else hipExtLaunchKernelGGL(k_step<N, MODE_FULL>, grid_full, block, 0, s, ev0, ev1, 0, p);
         break;
     case MODE_IO: BB_LAUNCH(MODE_IO); break;
     case MODE_IO_OBS: BB_LAUNCH(MODE_IO_OBS); break;
