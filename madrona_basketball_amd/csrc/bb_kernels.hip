@@ -400,6 +400,33 @@ struct LaneOrig {
 };
 static_assert(sizeof(LaneOrig) <= 4 * 52, "fits a row of the observation tile");
 
+// Words a lane parks in the observation tile until its observation pass,
+// word-major (word i of lane l at tile[i * WAVE + l]): each ds_write_b32 /
+// ds_read_b32 then covers 32 consecutive banks per lane group.  Lane-major at
+// the tile's row stride (52 or 68 dwords, 4 mod 8) they were 4-way bank
+// conflicts, most of k_step<2>'s SQ_LDS_BANK_CONFLICT.
+template <class X>
+__device__ __forceinline__ void park_words(float *tile, int lane, const X &x)
+{
+    static_assert(sizeof(X) % 4 == 0, "whole words");
+    uint32_t u[sizeof(X) / 4];
+    __builtin_memcpy(u, &x, sizeof(X));
+    uint32_t *t = (uint32_t *)tile;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(X) / 4); i++) t[i * WAVE + lane] = u[i];
+}
+template <class X>
+__device__ __forceinline__ X unpark_words(const float *tile, int lane)
+{
+    uint32_t u[sizeof(X) / 4];
+    const uint32_t *t = (const uint32_t *)tile;
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(X) / 4); i++) u[i] = t[i * WAVE + lane];
+    X x;
+    __builtin_memcpy(&x, u, sizeof(X));
+    return x;
+}
+
 // Observation rows of the agent-lane kernel into obs (a [W][N][OBSW] base):
 // the lane's intrinsic block, exchanged with the world's lanes by DPP, then
 // the row through the LDS tile (fast rows) or directly (slow rows).
@@ -470,9 +497,9 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     World<N> v;  // the world with this lane's agent in slot 0
     trace_point<MODE>(p, 0);
     // The event-only words as loaded (store only on change, see Orig) wait
-    // in the lane's row of the observation tile, which is free until the
-    // observation pass: registers stay with the systems.
-    LaneOrig *lo = (LaneOrig *)(tile + lane * T::RS);
+    // in the observation tile, which is free until the observation pass:
+    // registers stay with the systems.
+    static_assert(sizeof(LaneOrig) / 4 * WAVE <= T::FLOATS, "parked words fit the tile");
     if (active) {
         load_world(s, p, w);
         {
@@ -481,7 +508,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
             LaneOrig x;
             x.world = world_orig(o);
             x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
-            *lo = x;
+            park_words(tile, lane, x);
         }
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
@@ -493,7 +520,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         // reward + state columns first, so their stores drain while the
         // observation row is built
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
-        const LaneOrig x = *lo;
+        const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
         store_world_agent(v, p, w * N + k, 0, &x.agent);
         if (k == 0) {
             Orig<N> o;
@@ -544,7 +571,6 @@ __device__ __forceinline__ void step_agent_lanes_pipelined(const Params &p, floa
         World<N> s = nxt;
         World<N> v;
         Ctx c = make_ctx(p, w, k == 0);
-        LaneOrig *lo = (LaneOrig *)(tile + lane * T::RS);
         if (active) {
             {
                 Orig<N> o;
@@ -552,7 +578,7 @@ __device__ __forceinline__ void step_agent_lanes_pipelined(const Params &p, floa
                 LaneOrig x;
                 x.world = world_orig(o);
                 x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
-                *lo = x;
+                park_words(tile, lane, x);
             }
             if (next_ok) load_world(nxt, p, wn);
             step_world_pre_obs(s, c, ag);
@@ -563,7 +589,7 @@ __device__ __forceinline__ void step_agent_lanes_pipelined(const Params &p, floa
         if (active) {
             agent_view(s, v, k);
             sys_reward_agent(v, 0, AGENT0_ID + k);
-            const LaneOrig x = *lo;
+            const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
             store_world_agent(v, p, w * N + k, 0, &x.agent);
             if (k == 0) {
                 Orig<N> o;
@@ -594,7 +620,7 @@ template <int N>
 __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile)
 {
     using T = RolloutTile<N>;
-    static_assert(T::RS >= 6, "a tile row parks the lane's staged action row");
+    static_assert(6 * WAVE <= T::FLOATS, "the tile parks the lanes' staged action rows");
     const int lane = threadIdx.x;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
     const int64_t w = w0 + lane / N;
@@ -636,7 +662,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
         c.erf_tab = erf_tab;
         const LaneAgents<N, MODE_FULL> ag{k, &p};
         int32_t *act_t = r.actions + (int64_t)t * rows * 6;
-        uint32_t *park = (uint32_t *)(tile + lane_t * T::RS);  // idle until the observation pass
+        uint32_t *park = (uint32_t *)tile + lane_t;  // word q at park[q * WAVE]: idle until the observation pass
         int32_t ib = -1;
         bool share = false;
         if (active) {
@@ -647,7 +673,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
 #pragma unroll
                 for (int q = 0; q < 6; q++) s.act[i][q] = (int32_t)a_next[6 * i + q];
 #pragma unroll
-            for (int q = 0; q < 6; q++) park[q] = (uint32_t)pick_by<N>(k, [&](int j) { return s.act[j][q]; });
+            for (int q = 0; q < 6; q++) park[q * WAVE] = (uint32_t)pick_by<N>(k, [&](int j) { return s.act[j][q]; });
             // (unconditional -- the last step re-reads its own rows -- so that
             // every path through the loop has the same loads in flight)
             load_words<6 * N>(t + 1 < r.steps ? act_t + rows * 6 : act_t, w_t, a_next);
@@ -669,7 +695,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
             // the defence AI's overrides go back into the staged rows
             bool changed = false;
 #pragma unroll
-            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q];
+            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
             if (changed) {
                 uint32_t a[6];
 #pragma unroll
