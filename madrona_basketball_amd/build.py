@@ -18,9 +18,15 @@ AGENT_COUNTS = [2, 4, 6, 8, 10]
 # k_rollout's step loop and then spills them (628 B/lane of scratch); without
 # it they are rematerialised in place.  k_step is unaffected (same VGPRs).
 KERNEL_FLAGS = ["-mllvm", "-disable-machine-licm"]
+# Per agent count: the max-ILP machine scheduler for the N = 2 agent-lane
+# kernels (A/B, profiles/r02/t_flags_ab.txt: k_step<2> 21.7-21.8 -> 21.5 us at
+# 65 536 worlds, 13.1 -> 12.8 us at 8 192); the shared-world kernels (N >= 4)
+# keep the default (N = 4 68.4 vs 68.5 us).
+N_FLAGS = {2: ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 # (source, extra flags, object name): the step kernel once per agent count,
 # compiled in parallel
-UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}", *KERNEL_FLAGS], f"bb_kernels_n{n}.o") for n in AGENT_COUNTS]
+UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}", *KERNEL_FLAGS, *N_FLAGS.get(n, [])], f"bb_kernels_n{n}.o")
+          for n in AGENT_COUNTS]
          + [("bb_common.hip", [], "bb_common.o"), ("bb_host.hip", [], "bb_host.o"),
             ("bb_policy.hip", [], "bb_policy.o")])
 SOURCES = sorted({u[0] for u in UNITS})
