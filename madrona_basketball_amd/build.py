@@ -20,9 +20,12 @@ AGENT_COUNTS = [2, 4, 6, 8, 10]
 KERNEL_FLAGS = ["-mllvm", "-disable-machine-licm"]
 # Per agent count: the max-ILP machine scheduler for the N = 2 agent-lane
 # kernels (A/B, profiles/r02/t_flags_ab.txt: k_step<2> 21.7-21.8 -> 21.5 us at
-# 65 536 worlds, 13.1 -> 12.8 us at 8 192); the shared-world kernels (N >= 4)
-# keep the default (N = 4 68.4 vs 68.5 us).
-N_FLAGS = {2: ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# 65 536 worlds, 13.1 -> 12.8 us at 8 192; K=32 rollout 518-535 -> 485 us).
+# The shared-world kernels (N >= 4) keep the default: N = 6 and 10 looked
+# 1-2 % faster in one A/B (t_ilp_shared_ab.txt) but not on a second box
+# (r02v: 141.1 / 310.5 us), N = 4 and 8 were slower.
+MAX_ILP = ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+N_FLAGS = {2: MAX_ILP}
 # (source, extra flags, object name): the step kernel once per agent count,
 # compiled in parallel
 UNITS = ([("bb_kernels.hip", [f"-DBB_N={n}", *KERNEL_FLAGS, *N_FLAGS.get(n, [])], f"bb_kernels_n{n}.o")
