@@ -20,7 +20,8 @@ AGENT_COUNTS = [2, 4, 6, 8, 10]
 KERNEL_FLAGS = ["-mllvm", "-disable-machine-licm"]
 # Per agent count: the max-ILP machine scheduler for the N = 2 agent-lane
 # kernels (A/B, profiles/r02/t_flags_ab.txt: k_step<2> 21.7-21.8 -> 21.5 us at
-# 65 536 worlds, 13.1 -> 12.8 us at 8 192; K=32 rollout 518-535 -> 485 us).
+# 65 536 worlds, 13.1 -> 12.8 us at 8 192; K=32 rollout 518-535 -> 485 us;
+# max-memory-clause and iterative-ilp are slower, v_sched_strategy_ab.txt).
 # The shared-world kernels (N >= 4) keep the default: N = 6 and 10 looked
 # 1-2 % faster in one A/B (t_ilp_shared_ab.txt) but not on a second box
 # (r02v: 141.1 / 310.5 us), N = 4 and 8 were slower.
