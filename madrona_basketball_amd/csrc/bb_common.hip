@@ -111,6 +111,29 @@ __global__ __launch_bounds__(256) void k_stream_probe(const float4 *src, float4 
     }
 }
 
+// Diagnostics (tests/test_gpu_math.py): the step's scalar math evaluated on
+// gfx950 over caller inputs, to compare bit for bit with the host build of
+// the same header.  fn: 0 sinf, 1 cosf, 2 atanf, 3 acosf, 4 atan2f(x, y),
+// 5 (float)erf_d, 6 acos_d(c) > pi/8 as 0/1, 7 (float)(-1 + exp_d(x)).
+__global__ __launch_bounds__(256) void k_math_probe(int fn, const float *x, const float *y, float *out, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float v = x[i];
+    float r;
+    switch (fn) {
+    case 0: r = bbm::sinf_(v); break;
+    case 1: r = bbm::cosf_(v); break;
+    case 2: r = bbm::atanf_(v); break;
+    case 3: r = bbm::acosf_(v); break;
+    case 4: r = bbm::atan2f_(v, y[i]); break;
+    case 5: r = (float)bbm::erf_d((double)v); break;
+    case 6: r = ((float)bbm::acos_d((double)v) > PI_OVER_8) ? 1.f : 0.f; break;
+    default: r = (float)(-1.0 + bbm::exp_d((double)v)); break;
+    }
+    out[i] = r;
+}
+
 static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
 
 template <int N>
@@ -137,6 +160,14 @@ hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uin
     const int64_t total = (int64_t)count * a.off[RECORD_SEGS];
     if (total <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_record, grid_for(total, 256), dim3(256), 0, s, a, world0, total, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_math_probe(int fn, const float *x, const float *y, float *out, int64_t n, hipStream_t s)
+{
+    if (fn < 0 || fn > 7 || n < 0) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_math_probe, grid_for(n, 256), dim3(256), 0, s, fn, x, y, out, n);
     return hipGetLastError();
 }
 

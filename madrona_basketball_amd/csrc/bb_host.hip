@@ -834,6 +834,18 @@ int bb_diag_trace(bb_sim *s, void *stream, uint64_t *out, int64_t max_waves, int
     return BB_OK;
 }
 
+// Diagnostic (not in the public header): out[i] = f(x[i]) (or f(x[i], y[i]))
+// of the step's scalar math on the device (bb_common.hip k_math_probe), for
+// bit-for-bit comparison with the host build of bb_math.h.
+int bb_diag_math(int32_t fn, const float *x, const float *y, float *out, int64_t n, int32_t gpu_id, void *stream)
+{
+    if (!x || !out || n < 0 || (fn == 4 && !y)) return fail(BB_ERR_INVALID_ARG, "bb_diag_math");
+    DeviceGuard g(gpu_id);
+    hipError_t e = bb::launch_math_probe(fn, x, y, out, n, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "launch math probe");
+    return BB_OK;
+}
+
 int64_t bb_algorithmic_bytes_per_world(int32_t n)
 {
     // B(N) = N (268 + 4 obs_used(N)) + 152

@@ -288,6 +288,9 @@ struct LaneAgents {
         static_assert(N == G, "one lane per agent");
         if constexpr (OWN_APPLY) {
             apply(k, f(k));
+            // the next system reads the other lanes' LDS writes: a workgroup
+            // barrier orders them (the block is one wave, so it costs ~nothing)
+            __syncthreads();
         } else {
             decltype(f(0)) out[G];
             lane_gather<G>(f(k), out);

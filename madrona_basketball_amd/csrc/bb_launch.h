@@ -74,6 +74,8 @@ hipError_t launch_policy(const PolicyArgs &a, hipStream_t s);
 void host_policy(const PolicyArgs &a);
 hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s);
 void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);
+// diagnostics: the step's scalar math on the device (bb_diag_math)
+hipError_t launch_math_probe(int fn, const float *x, const float *y, float *out, int64_t n, hipStream_t s);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)
 hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, int pattern,
                                int nt, hipStream_t s);

@@ -59,6 +59,7 @@ static constexpr double INV_LN2 = 1.44269504088896338700e+00;
 static constexpr double LN2_HI = 6.93147180369123816490e-01;
 static constexpr double LN2_LO = 1.90821492927058770002e-10;
 static constexpr double TWO_OVER_SQRTPI = 1.1283791670955126;   // 2/sqrt(pi)
+static constexpr double TWO_OVER_SQRTPI_M1 = 1.28379167095512586316e-01;  // 2/sqrt(pi) - 1
 static constexpr double INV_SQRTPI = 0.5641895835477563;        // 1/sqrt(pi)
 
 // ---------------------------------------------------------------- atan family
@@ -233,12 +234,18 @@ BB_HD double erf_d(double x, const double *tab = &ERF_TAYLOR[0][0])
     const double ax = fabs_d(x);
     double r;
     if (ax < 0.75) {
-        // erf x = 2/sqrt(pi) * x * sum_n (-1)^n z^n / (n! (2n+1)), z = x^2
+        // erf x = 2/sqrt(pi) * x * sum_n (-1)^n z^n / (n! (2n+1)), z = x^2,
+        // evaluated as x + x*y with y = (2/sqrt(pi) - 1) + 2/sqrt(pi) z q(z)
+        // (q: the series from n = 1 on): the leading x is exact and one fma
+        // rounds the sum, so (float)erf_d equals glibc's (float)erf on every
+        // float below 0.75 (tests/test_math.py, exhaustive; the plain product
+        // form differed on one input, 1.8398030e-4).
         const double z = ax * ax;
-        double p = ERF_COEF.c[ERF_NT - 1];
+        double q = ERF_COEF.c[ERF_NT - 1];
 #pragma unroll
-        for (int n = ERF_NT - 2; n >= 0; n--) p = fma_d(p, z, ERF_COEF.c[n]);
-        r = TWO_OVER_SQRTPI * (ax * p);
+        for (int n = ERF_NT - 2; n >= 1; n--) q = fma_d(q, z, ERF_COEF.c[n]);
+        const double y = fma_d(TWO_OVER_SQRTPI * z, q, TWO_OVER_SQRTPI_M1);
+        r = fma_d(ax, y, ax);
     } else if (ax < 4.0) {
         const int k = (int)((ax - 0.75) * 4.0);
         const double t = ax - (0.875 + 0.25 * (double)k);  // exact, |t| <= 1/8
@@ -268,6 +275,17 @@ BB_HD double erf_d(double x, const double *tab = &ERF_TAYLOR[0][0])
 //     operation rounding on its own (-ffp-contract=off).
 // Constants are the words the library holds.  Pinned exhaustively (every
 // float input) against the host's libm by tests/test_math.py.
+//
+// Attribution.  The atanf / atan2f / acosf algorithms and constants below
+// follow fdlibm (float versions by Ian Lance Taylor, Cygnus Support), whose
+// notice reads:
+//   Copyright (C) 1993 by Sun Microsystems, Inc. All rights reserved.
+//   Developed at SunPro, a Sun Microsystems, Inc. business.
+//   Permission to use, copy, modify, and distribute this software is freely
+//   granted, provided that this notice is preserved.
+// The sinf / cosf algorithm and its __sincosf_table coefficients are those of
+// glibc's sysdeps/ieee754/flt-32 (Szabolcs Nagy, ARM Ltd; contributed to glibc
+// from ARM's optimized-routines), here restated, not copied.
 BB_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
 BB_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 BB_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }

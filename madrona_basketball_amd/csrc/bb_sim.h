@@ -346,12 +346,16 @@ BB_HD void store_words(void *base, int64_t w, const uint32_t (&o)[NW])
     uint32_t *p = (uint32_t *)base + w * NW;
 #if defined(__HIP_DEVICE_COMPILE__)
     if constexpr (AUX >= 0) {
-        // descriptor at the first active lane's chunk (wave-uniform); the
-        // other lanes' chunks follow it (w grows with the lane), so the
-        // 32-bit offsets stay small at any column size
+        // Wave-uniform descriptor 63 chunks below the first active lane's
+        // chunk: a lane's offset (w - wf + 63 chunks) is >= 0 for any lane
+        // whose chunk lies at most 63 chunks before the first active lane's
+        // -- every caller's lanes store chunks of the wave's own <= 64 rows,
+        // in whatever lane order -- and stays small at any column size.
+        // (Only the descriptor's base address may lie before the column; no
+        // access does.)
         const uint64_t wu = (uint64_t)w;
         const int64_t wf = (int64_t)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wu >> 32)) << 32) |
-                                     __builtin_amdgcn_readfirstlane((uint32_t)wu));
+                                     __builtin_amdgcn_readfirstlane((uint32_t)wu)) - 63;
         const auto rs = __builtin_amdgcn_make_buffer_rsrc((uint32_t *)base + wf * NW, 0, 0x7fffffff, 0x00020000);
         const int off = (int)((w - wf) * NW * 4);
         typedef uint32_t u2 __attribute__((ext_vector_type(2)));

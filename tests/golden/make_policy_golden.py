@@ -43,6 +43,23 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 OUT = os.path.join(HERE, "policy_golden.npz")
 BUCKETS = [2, 8, 3, 2, 2, 2]
 SEED = 20261016
+# The reference modules this script imports (and so executes), pinned to the
+# contents they had when policy_golden.npz was generated: a changed file is
+# refused rather than run.
+REF_SHA256 = {
+    "agent.py": "8215be664e07b131f8751428bffe0c2ec0801bdc3d2214a82d8b4c1685bff67e",
+    "action.py": "b1511f622fb76412bc9ec869c22f3891f94ea06b90710e9add49e5ed9ad156e8",
+    "moving_avg.py": "dfe803c863899f22162fcdbd86930506563e8e1c6d0f1873e26d886911c8c966",
+}
+
+
+def check_reference_files() -> None:
+    import hashlib
+    for name, want in REF_SHA256.items():
+        with open(os.path.join(REF_SCRIPTS, name), "rb") as f:
+            got = hashlib.sha256(f.read()).hexdigest()
+        if got != want:
+            raise SystemExit(f"refusing to import {REF_SCRIPTS}/{name}: sha256 {got} != pinned {want}")
 
 
 def observation_rows(worlds: int = 256, steps: int = 150) -> np.ndarray:
@@ -56,6 +73,7 @@ def observation_rows(worlds: int = 256, steps: int = 150) -> np.ndarray:
 
 def main():
     obs_np = observation_rows()
+    check_reference_files()
     sys.path.insert(0, REF_SCRIPTS)
     from action import DiscreteActionDistributions  # noqa: E402  (reference module)
     from agent import Agent  # noqa: E402  (reference module)

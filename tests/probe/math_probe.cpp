@@ -19,6 +19,10 @@ VEC1(glibc_cosf, cosf(v))
 VEC1(glibc_atanf, atanf(v))
 VEC1(glibc_acosf, acosf(v))
 VEC1(cr_sinf, (float)sin((double)v))
+// the device probe's float-valued forms of the double functions (bb_diag_math 5-7)
+VEC1(bb_erff, (float)bbm::erf_d((double)v))
+VEC1(bb_acospred, ((float)bbm::acos_d((double)v) > 3.14159265358979323846f / 8.f) ? 1.f : 0.f)
+VEC1(bb_expm1sum, (float)(-1.0 + bbm::exp_d((double)v)))
 void bb_atan2f(const float *y, const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = bbm::atan2f_(y[i], x[i]); }
 void glibc_atan2f(const float *y, const float *x, float *out, int64_t n) { for (int64_t i = 0; i < n; i++) out[i] = atan2f(y[i], x[i]); }
 #define VECD(name, expr) \
@@ -66,6 +70,70 @@ int64_t exhaustive_mismatches(int fn, int threads, uint32_t *first)
                 }
                 }
                 if (!ok && bad[t]++ == 0) f[t] = u;
+            }
+        });
+    }
+    for (auto &th : pool) th.join();
+    int64_t n = 0;
+    *first = 0;
+    for (int t = 0; t < threads; t++) {
+        if (bad[t] && !n) *first = f[t];
+        n += bad[t];
+    }
+    return n;
+}
+
+// The double functions of the step take a float argument and their result
+// ends in a float (or a float comparison), so their agreement with glibc is
+// decidable input by input.  Over the 32-bit patterns [lo, hi):
+//   5  erf : (float)erf_d((double)x) == (float)erf((double)x)    (game.cpp:808)
+//   6  exp : exp_d((double)x) == exp((double)x), as doubles       (game.cpp:868)
+//   7  acos: ((float)acos_d((double)c) > pi/8) == ((float)acos((double)c) > pi/8)
+//                                                                  (game.cpp:746-747)
+//   8  exp : (float)((double)r + exp_d(x)) == (float)((double)r + exp(x)) for the
+//            reward bases r the step can hold there (see tests/test_math.py)
+static bool double_check(int fn, float x)
+{
+    switch (fn) {
+    case 5: return same_bits((float)bbm::erf_d((double)x), (float)erf((double)x));
+    case 6: {
+        const double a = bbm::exp_d((double)x), b = exp((double)x);
+        uint64_t ua, ub;
+        memcpy(&ua, &a, 8);
+        memcpy(&ub, &b, 8);
+        return ua == ub || (a != a && b != b);
+    }
+    case 7: {
+        const float pi8 = 3.14159265358979323846f / 8.f;
+        return ((float)bbm::acos_d((double)x) > pi8) == ((float)acos((double)x) > pi8);
+    }
+    default: {
+        const double a = bbm::exp_d((double)x), b = exp((double)x);
+        if (a == b) return true;
+        // reward before the exp term: -1 + (the tag / out-of-bounds / clock
+        // terms of that step): 0, +-10, -100, +10 - 10, ...
+        static const float base[] = {-1.f, -11.f, 9.f, -101.f, -111.f, -91.f, 19.f, -21.f};
+        for (float r : base)
+            if (!same_bits((float)((double)r + a), (float)((double)r + b))) return false;
+        return true;
+    }
+    }
+}
+
+int64_t exhaustive_double_mismatches(int fn, int threads, uint32_t lo, uint32_t hi, uint32_t *first)
+{
+    std::vector<int64_t> bad(threads, 0);
+    std::vector<uint32_t> f(threads, 0);
+    std::vector<std::thread> pool;
+    const uint64_t total = (uint64_t)hi - lo, chunk = total / threads;
+    for (int t = 0; t < threads; t++) {
+        pool.emplace_back([&, t] {
+            const uint64_t a = lo + chunk * t, b = t + 1 == threads ? (uint64_t)hi : a + chunk;
+            for (uint64_t i = a; i < b; i++) {
+                float x;
+                const uint32_t u = (uint32_t)i;
+                memcpy(&x, &u, 4);
+                if (!double_check(fn, x) && bad[t]++ == 0) f[t] = u;
             }
         });
     }

@@ -10,8 +10,9 @@ MATH_LIBM mode -- the literal glibc float calls, i.e. the reference CPU
 executor's arithmetic -- and the HIP path must meet the north_star bar against
 it (BASELINE.json): integer / score / done state bit-exact, floats within 1e-5
 (tests/helpers.py), for identical action sequences.  Since bb_math.h restates
-glibc's float functions operation for operation, the columns are in fact
-asserted bit-identical.
+glibc's float functions operation for operation (and its erf / exp / acos
+round like glibc's on every float input the step reaches), the columns are
+expected bit-identical; that fraction is reported beside the asserted bar.
 
 Each case reports the bit-identical fraction of every column (printed, and
 collected into gpurun_out/libm_parity.json when that directory exists).
@@ -65,6 +66,12 @@ def test_gpu_vs_reference_cpu_math(case):
     if os.path.isdir(OUT):
         with open(os.path.join(OUT, "libm_parity.jsonl"), "a") as f:
             f.write(json.dumps(report) + "\n")
-    # beyond the north_star tolerance: bb_math.h restates glibc's float
-    # functions exactly, so every word of every column is expected identical
-    assert min(worst.values()) == 1.0, {k: v for k, v in worst.items() if v < 1.0}
+    # The assertion is the north_star bar, checked inside run_lockstep at
+    # every 50th step: integer / score / done columns exact, floats within
+    # 1e-5 (tests/helpers.py).  The bit-identical fraction is reported, not
+    # asserted: it is expected to be 1.0 (bb_math.h restates glibc's float
+    # functions, and erf / exp / acos round like glibc's on every float the
+    # step reaches, tests/test_math.py), but a float that differed in its last
+    # bit would still be inside the bar.
+    print(f"{case}: min bit-identical fraction {min(worst.values()):.9f} "
+          f"({sum(v < 1.0 for v in worst.values())} columns below 1.0)")

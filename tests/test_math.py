@@ -5,27 +5,16 @@ every input; the double functions (erf/exp/acos, rounded to float by the
 reference) within a few double ulps (DESIGN.md "Numerics")."""
 import ctypes
 import os
-import subprocess
 
 import numpy as np
 import pytest
 
-HERE = os.path.dirname(os.path.abspath(__file__))
-SRC = os.path.join(HERE, "probe", "math_probe.cpp")
-LIB = os.path.join(HERE, "probe", "libmath_probe.so")
+from tests.math_probe import load_math_probe
 
 
 @pytest.fixture(scope="module")
 def P():
-    hdr = os.path.join(HERE, "..", "madrona_basketball_amd", "csrc", "bb_math.h")
-    if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(hdr)):
-        # -mfma (where the CPU has it) only speeds up fma_d; fma is exact either way
-        fma = ["-mfma"] if "fma" in open("/proc/cpuinfo").read().split() else []
-        subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
-                        *fma, "-pthread", "-o", LIB, SRC, "-lm"], check=True)
-    L = ctypes.CDLL(LIB)
-    L.exhaustive_mismatches.restype = ctypes.c_int64
-    return L
+    return load_math_probe()
 
 
 def call(P, name, x, dtype=np.float32):
@@ -127,3 +116,43 @@ def test_glibc_float_functions_are_not_correctly_rounded(P):
     x = inputs(-50, 50, seed=7)
     frac = (call(P, "glibc_sinf", x) != call(P, "cr_sinf", x)).mean()
     assert 0 < frac < 0.05, frac
+
+
+def _fbits(x: float) -> int:
+    return int(np.array([x], np.float32).view(np.uint32)[0])
+
+
+# (check id of math_probe.cpp exhaustive_double_mismatches, [lo, hi) of 32-bit patterns)
+_DOUBLE_DOMAINS = {
+    # (float)erf((double)x) over every float (game.cpp:808 rounds it to float)
+    "erf_pos": (5, 0x00000000, 0x7F800001),
+    "erf_neg": (5, 0x80000000, 0xFF800001),
+    # acos(c) > pi/8 for every float c in [-1, 1] (game.cpp:746-747; the step
+    # compares c against the threshold Params.rot_thresh derived from acos_d)
+    "acos_pred_pos": (7, 0x00000000, _fbits(1.0) + 1),
+    "acos_pred_neg": (7, 0x80000000, _fbits(-1.0) + 1),
+    # reward += exp(-0.4 dist) (game.cpp:868): every float x in [-104, 0]
+    # (below that both are 0), summed onto the rewards a defender can hold
+    # at that point of the step
+    "exp_reward": (8, 0x80000000, _fbits(-104.0) + 1),
+}
+
+
+@pytest.mark.parametrize("dom", list(_DOUBLE_DOMAINS))
+def test_double_functions_round_like_glibc_on_every_float(P, dom):
+    """The step's double functions take a float and end in a float (or a
+    float comparison): their float outcome equals glibc's on every input of
+    the domain the step reaches (exhaustive), so the HIP path is bit-exact
+    against the reference CPU executor's erf / acos / exp."""
+    fn, lo, hi = _DOUBLE_DOMAINS[dom]
+    first = ctypes.c_uint32()
+    n = P.exhaustive_double_mismatches(fn, _threads(), lo, hi, ctypes.byref(first))
+    assert n == 0, (dom, n, hex(first.value))
+
+
+def test_exp_d_is_not_glibc_exp_in_double(P):
+    """exp_d is not glibc's exp bit for bit in double (so the reward check
+    above is on the float sums the step forms, not on the doubles)."""
+    first = ctypes.c_uint32()
+    n = P.exhaustive_double_mismatches(6, _threads(), 0x80000000, _fbits(-1.0), ctypes.byref(first))
+    assert n > 0
