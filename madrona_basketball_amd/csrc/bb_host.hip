@@ -9,9 +9,14 @@
 // except creation and the optional kernel timing of bb_step_n.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -104,8 +109,11 @@ int validate(const bb_config *cfg)
 
 int host_threads_for(int64_t worlds)
 {
+    // default: the machine's threads, at most 16 (a GPU box's CPU share);
+    // BB_CPU_THREADS overrides
     const char *env = std::getenv("BB_CPU_THREADS");
     int t = env ? std::atoi(env) : (int)std::thread::hardware_concurrency();
+    if (!env && t > 16) t = 16;
     if (t < 1) t = 1;
     const int64_t max_useful = (worlds + 255) / 256;
     if (t > max_useful) t = (int)max_useful;
@@ -130,6 +138,95 @@ struct DeviceGuard {
 
 }  // namespace
 
+namespace bb {
+
+// Persistent worker pool of the host executor (ExecMode.CPU), the stand-in
+// for the reference's CPU TaskGraphExecutor worker threads (src/mgr.cpp:49-81:
+// created once with the Manager, reused every step).  run(f) calls f(t) for
+// t = 0..size-1 on the workers -- the calling thread is worker 0 -- and
+// returns when all are done.  Workers spin briefly, then sleep on a condition
+// variable, between jobs.
+class HostPool {
+public:
+    explicit HostPool(int n) : n_(n < 1 ? 1 : n)
+    {
+        for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { worker(t); });
+    }
+    ~HostPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(m_);
+            stop_ = true;
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return n_; }
+    void run(const std::function<void(int)> &f)
+    {
+        if (n_ == 1) { f(0); return; }
+        {
+            std::lock_guard<std::mutex> g(m_);
+            job_ = &f;
+            left_.store(n_ - 1, std::memory_order_relaxed);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        f(0);
+        // the others: spin, then sleep
+        for (int i = 0; left_.load(std::memory_order_acquire) != 0; i++) {
+            if (i > 4096) {
+                std::unique_lock<std::mutex> g(m_);
+                done_cv_.wait(g, [this] { return left_.load(std::memory_order_acquire) == 0; });
+                break;
+            }
+            std::this_thread::yield();
+        }
+        job_ = nullptr;
+    }
+
+private:
+    void worker(int t)
+    {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g = gen_.load(std::memory_order_acquire);
+            for (int i = 0; g == seen && i < 4096; i++) {
+                std::this_thread::yield();
+                g = gen_.load(std::memory_order_acquire);
+            }
+            if (g == seen) {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                g = gen_.load(std::memory_order_acquire);
+            }
+            seen = g;
+            const std::function<void(int)> *job;
+            {
+                std::lock_guard<std::mutex> lk(m_);
+                if (stop_) return;
+                job = job_;
+            }
+            (*job)(t);
+            if (left_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+                std::lock_guard<std::mutex> lk(m_);
+                done_cv_.notify_one();
+            }
+        }
+    }
+    const int n_;
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> left_{0};
+    const std::function<void(int)> *job_ = nullptr;
+    bool stop_ = false;
+};
+
+}  // namespace bb
+
 struct bb_sim {
     bb_config cfg;
     int n = 2;
@@ -137,6 +234,7 @@ struct bb_sim {
     bool owns = false;
     void *slot[NUM_SLOTS] = {};
     bb::Params p;
+    std::unique_ptr<bb::HostPool> pool;  // ExecMode.CPU workers (created with the simulator)
 };
 
 namespace {
@@ -277,6 +375,7 @@ int create_common(const bb_config *cfg, void *const *bufs, int32_t nbuf, bb_sim 
         }
     }
     bind_params(s);
+    if (cfg->exec_mode == BB_EXEC_CPU) s->pool.reset(new bb::HostPool(host_threads_for(cfg->num_worlds)));
     rc = init_worlds(s);
     if (rc != BB_OK) {
         bb_destroy(s);
@@ -297,21 +396,23 @@ static void host_range(const Params &p, int64_t lo, int64_t hi)
     for (int64_t w = lo; w < hi; w++) step_one_world<N>(p, w);
 }
 
+// One step of every world on the pool: worker t steps worlds [W t/T, W (t+1)/T).
+// With `actions` (random_actions != 0) each worker first writes its own worlds'
+// synthetic action rows -- worlds are independent, so no barrier between the
+// two.
 template <int N>
-static int host_step_n(const Params &p, int threads)
+static int host_step_n(const Params &p, HostPool &pool, bool actions, uint32_t seed, uint32_t step)
 {
     const int64_t W = p.num_worlds;
-    if (threads <= 1) {
-        host_range<N>(p, 0, W);
-        return BB_OK;
-    }
-    std::vector<std::thread> pool;
-    pool.reserve((size_t)threads);
-    for (int t = 0; t < threads; t++) {
-        const int64_t lo = W * t / threads, hi = W * (t + 1) / threads;
-        pool.emplace_back([&p, lo, hi] { host_range<N>(p, lo, hi); });
-    }
-    for (auto &th : pool) th.join();
+    const int T = pool.size();
+    pool.run([&](int t) {
+        const int64_t lo = W * t / T, hi = W * (t + 1) / T;
+        if (actions)
+            for (int64_t w = lo; w < hi; w++)
+                for (int a = 0; a < N; a++)
+                    random_action(seed, step, (uint32_t)(p.world_offset + w), (uint32_t)a, p.c.action + (w * N + a) * 6);
+        host_range<N>(p, lo, hi);
+    });
     return BB_OK;
 }
 
@@ -322,14 +423,14 @@ static int host_init_n(const Params &p)
     return BB_OK;
 }
 
-int host_step(int n, const Params &p, int threads)
+int host_step(int n, const Params &p, HostPool &pool, bool actions, uint32_t seed, uint32_t step)
 {
     switch (n) {
-    case 2: return host_step_n<2>(p, threads);
-    case 4: return host_step_n<4>(p, threads);
-    case 6: return host_step_n<6>(p, threads);
-    case 8: return host_step_n<8>(p, threads);
-    case 10: return host_step_n<10>(p, threads);
+    case 2: return host_step_n<2>(p, pool, actions, seed, step);
+    case 4: return host_step_n<4>(p, pool, actions, seed, step);
+    case 6: return host_step_n<6>(p, pool, actions, seed, step);
+    case 8: return host_step_n<8>(p, pool, actions, seed, step);
+    case 10: return host_step_n<10>(p, pool, actions, seed, step);
     default: return BB_ERR_UNSUPPORTED;
     }
 }
@@ -346,11 +447,15 @@ int host_init(int n, const Params &p)
     }
 }
 
-int host_random_actions(int n, const Params &p, uint32_t seed, uint32_t step)
+int host_random_actions(int n, const Params &p, HostPool &pool, uint32_t seed, uint32_t step)
 {
-    for (int64_t w = 0; w < p.num_worlds; w++)
-        for (int a = 0; a < n; a++)
-            random_action(seed, step, (uint32_t)(p.world_offset + w), (uint32_t)a, p.c.action + (w * n + a) * 6);
+    const int64_t W = p.num_worlds;
+    const int T = pool.size();
+    pool.run([&](int t) {
+        for (int64_t w = W * t / T; w < W * (t + 1) / T; w++)
+            for (int a = 0; a < n; a++)
+                random_action(seed, step, (uint32_t)(p.world_offset + w), (uint32_t)a, p.c.action + (w * n + a) * 6);
+    });
     return BB_OK;
 }
 
@@ -427,7 +532,7 @@ int bb_step(bb_sim *s, void *stream)
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
         return BB_OK;
     }
-    return bb::host_step(s->n, s->p, host_threads_for(s->cfg.num_worlds));
+    return bb::host_step(s->n, s->p, *s->pool);
 }
 
 int bb_write_random_actions(bb_sim *s, uint32_t action_seed, uint32_t step, void *stream)
@@ -439,7 +544,7 @@ int bb_write_random_actions(bb_sim *s, uint32_t action_seed, uint32_t step, void
         if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
         return BB_OK;
     }
-    return bb::host_random_actions(s->n, s->p, action_seed, step);
+    return bb::host_random_actions(s->n, s->p, *s->pool, action_seed, step);
 }
 
 int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed, uint32_t step0,
@@ -449,8 +554,7 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
     if (n < 0) return fail(BB_ERR_INVALID_ARG, "n must be >= 0");
     if (s->cfg.exec_mode != BB_EXEC_CUDA) {
         for (int32_t k = 0; k < n; k++) {
-            if (random_actions) bb::host_random_actions(s->n, s->p, action_seed, step0 + (uint32_t)k);
-            int rc = bb::host_step(s->n, s->p, host_threads_for(s->cfg.num_worlds));
+            int rc = bb::host_step(s->n, s->p, *s->pool, random_actions != 0, action_seed, step0 + (uint32_t)k);
             if (rc != BB_OK) return rc;
         }
         if (kernel_ms) *kernel_ms = 0.f;
@@ -504,7 +608,7 @@ int bb_fill_random_actions(bb_sim *s, int32_t *actions, int32_t n, uint32_t acti
             hipError_t e = bb::launch_random_actions(s->n, pp, action_seed, step0 + (uint32_t)k, (hipStream_t)stream);
             if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
         } else {
-            int rc = bb::host_random_actions(s->n, pp, action_seed, step0 + (uint32_t)k);
+            int rc = bb::host_random_actions(s->n, pp, *s->pool, action_seed, step0 + (uint32_t)k);
             if (rc != BB_OK) return rc;
         }
     }
@@ -519,7 +623,7 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     if (s->cfg.exec_mode != BB_EXEC_CUDA) {
         for (int32_t k = 0; k < n; k++) {
             pp.c.action = actions + (int64_t)k * rows;
-            int rc = bb::host_step(s->n, pp, host_threads_for(s->cfg.num_worlds));
+            int rc = bb::host_step(s->n, pp, *s->pool);
             if (rc != BB_OK) return rc;
         }
         if (n > 0) std::memcpy(s->p.c.action, actions + (int64_t)(n - 1) * rows, (size_t)rows * 4);
@@ -596,7 +700,7 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
     };
     if (s->cfg.exec_mode != BB_EXEC_CUDA) {
         for (int32_t k = 0; k < n; k++) {
-            int rc = bb::host_step(s->n, step_params(k), host_threads_for(s->cfg.num_worlds));
+            int rc = bb::host_step(s->n, step_params(k), *s->pool);
             if (rc != BB_OK) return rc;
         }
         std::memcpy(s->p.c.action, last_act, (size_t)rows * 24);

@@ -80,9 +80,12 @@ hipError_t launch_math_probe(int fn, const float *x, const float *y, float *out,
 hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, int pattern,
                                int nt, hipStream_t s);
 
-// Host executor (ExecMode.CPU): the same step code over a thread pool.
-int host_step(int n, const Params &p, int threads);
+// Host executor (ExecMode.CPU): the same step code over a persistent thread
+// pool (bb_host.hip HostPool); with `actions` each worker first writes the
+// synthetic action rows of its own worlds.
+class HostPool;
+int host_step(int n, const Params &p, HostPool &pool, bool actions = false, uint32_t seed = 0, uint32_t step = 0);
 int host_init(int n, const Params &p);
-int host_random_actions(int n, const Params &p, uint32_t seed, uint32_t step);
+int host_random_actions(int n, const Params &p, HostPool &pool, uint32_t seed, uint32_t step);
 
 }  // namespace bb
