@@ -24,6 +24,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "env steps/sec (whole node) at 65 536 worlds; 1→8 GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+EVENT_MIN_LAUNCHES = 200  # kernel-time averages over at least this many launches
 
 
 def log(*a):
@@ -127,9 +128,10 @@ def main():
                     help="diagnostics: rollouts without recorded outputs (each step rewrites the sim's own tensors)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end leg (env.py's step through Python: slice write, step, 3 clones)")
-    ap.add_argument("--no-beyond-cache", action="store_true",
-                    help="skip the 262144-world line (state beyond the 256 MiB Infinity Cache) reported beside "
-                         "the 65536-world headline")
+    ap.add_argument("--no-configs", "--no-beyond-cache", dest="no_configs", action="store_true",
+                    help="skip the lines of the other BASELINE configs (262144 x 2 beyond the Infinity Cache, "
+                         "8192 x 2 per step and K=32, the 32768 x 2 shard, 65536 x 4, 65536 x 10) reported "
+                         "beside the 65536-world headline")
     ap.add_argument("--dist", action="store_true",
                     help="start the process group (RCCL on the GPU) even at world size 1: exercises the "
                          "multi-rank barrier / max-reduce path on one device")
@@ -208,10 +210,11 @@ def main():
         lp = torch.empty((W,), dtype=torch.float32, device=dev)
         val = torch.empty((W,), dtype=torch.float32, device=dev)
 
-    def run(actions, time_kernels=False):
+    def run(actions, time_kernels=False, steps=None):
         """All staged steps: one step per launch, or chunks of K via bb_rollout."""
+        steps = args.steps if steps is None else steps
         if args.policy:  # actions come from the policy, not the staged rows
-            for t in range(args.steps):
+            for t in range(steps):
                 for a in range(args.agents):
                     pol.act(sim, a, lp, val, stochastic=True, seed=args.seed, step=t)
                 sim.step()
@@ -219,7 +222,7 @@ def main():
         if not K:
             return sim.step_n_staged(actions, time_kernels=time_kernels)
         ms = 0.0
-        for i in range(0, args.steps, K):
+        for i in range(0, steps, K):
             if args.no_record:
                 r = sim.rollout(actions[i:i + K], time_kernels=time_kernels)
             else:
@@ -237,17 +240,26 @@ def main():
     elapsed = max_over_ranks(elapsed)
 
     # kernel timing: the step kernel's own start/end (hipExtLaunchKernel
-    # events on the launch stream) over the same workload, re-staged
-    launches = args.steps // K if (K and fused) else args.steps
-    if on_gpu and not args.policy:
-        staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup + args.steps)
-        barrier()
-        kernel_ms = run(staged, time_kernels=True)
-        barrier()
-        avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / launches)
-    else:
-        avg_kernel_s = elapsed / launches
+    # events on the launch stream) over the same workload, re-staged; at
+    # least EVENT_MIN_LAUNCHES launches whatever --steps is, so the line's
+    # frac is an average as long as the committed rocprof summaries'
     del staged
+    if on_gpu and not args.policy:
+        per_launch = K if (K and fused) else 1
+        ev_steps = max(args.steps, EVENT_MIN_LAUNCHES * per_launch)
+        if K:
+            ev_steps = (ev_steps + K - 1) // K * K
+        staged = sim.stage_random_actions(ev_steps, action_seed=args.seed, step0=args.warmup + args.steps)
+        barrier()
+        kernel_ms = run(staged, time_kernels=True, steps=ev_steps)
+        barrier()
+        launches = ev_steps // per_launch
+        avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / launches)
+        del staged
+    else:
+        launches = args.steps // K if (K and fused) else args.steps
+        ev_steps = args.steps
+        avg_kernel_s = elapsed / launches
 
     # end-to-end leg (scripts/run.py:10-15 over scripts/env.py:147,167-170):
     # per step the trainee's int64 action rows are written into the action
@@ -281,33 +293,69 @@ def main():
                           "(env.py:147), SimpleGridworldSimulator.step() via ctypes, obs/reward/done "
                           "[:, 0].clone() (env.py:167-170); agent 1 acts through the hard-coded defence"}
 
-    # beside the headline: the same step at 262 144 worlds (1664 B of state
-    # and rows per world: 436 MB, beyond the 256 MiB Infinity Cache, where
-    # PMC traffic is HBM traffic), events-timed like the headline kernel
-    beyond = None
-    if (on_gpu and not args.no_beyond_cache and not args.policy and not K and world_size == 1
+    # beside the headline, every other BASELINE.json config as its own line:
+    # the same step at 262 144 worlds (1664 B of state and rows per world:
+    # 436 MB, beyond the 256 MiB Infinity Cache, where PMC traffic is HBM
+    # traffic), the C2 training batch (8 192 x 2, per step and as PPO's
+    # 32-step rollouts), the C4 per-GPU shard (32 768 x 2) and the "2v2" /
+    # "5v5" extensions (65 536 x 4 / x 10); each events-timed over
+    # >= EVENT_MIN_LAUNCHES launches like the headline kernel
+    extra = {}
+    if (on_gpu and not args.no_configs and not args.policy and not K and world_size == 1
             and W == 65536 and args.agents == 2):
-        W2, n2 = 262144, 100
-        sim2 = mba.SimpleGridworldSimulator(
-            discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
-            max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W2, gpu_id=dev.index,
-            num_agents=2, per_world_rng=True)
-        sim2.step_n(20, random_actions=True, action_seed=args.seed, step0=0)
-        acts2 = sim2.stage_random_actions(n2, action_seed=args.seed, step0=20)
-        sync()
-        t0 = time.perf_counter()
-        sim2.step_n_staged(acts2)
-        sync()
-        wall2 = time.perf_counter() - t0
-        acts2 = sim2.stage_random_actions(n2, action_seed=args.seed, step0=20 + n2)
-        sync()
-        k2 = sim2.step_n_staged(acts2, time_kernels=True) / 1e3 / n2
-        b2 = _lib.load().bb_algorithmic_bytes_per_world(2) * W2
-        beyond = {"worlds": W2, "steps": n2, "value": W2 * n2 / wall2, "unit": "env-steps/s",
-                  "kernel_avg_us": k2 * 1e6, "achieved": b2 / k2 / 1e9,
-                  "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(f"W{W2}_N2"),
-                  "algorithmic_bytes_per_launch": b2}
-        del sim2, acts2
+        L0 = _lib.load()
+
+        def config_line(W2, n2, K2=0, launches=EVENT_MIN_LAUNCHES):
+            steps2 = launches * (K2 or 1)
+            sim2 = mba.SimpleGridworldSimulator(
+                discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
+                max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W2, gpu_id=dev.index,
+                num_agents=n2, per_world_rng=True)
+            sim2.step_n(20, random_actions=True, action_seed=args.seed, step0=0)
+            bufs2 = sim2.rollout_buffers(K2) if K2 else None
+
+            def go(acts, timed):
+                if not K2:
+                    return sim2.step_n_staged(acts, time_kernels=timed)
+                ms = 0.0
+                for i in range(0, steps2, K2):
+                    ms += sim2.rollout(acts[i:i + K2], bufs2["obs"], bufs2["reward"], bufs2["done"],
+                                       time_kernels=timed) or 0.0
+                return ms
+            acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20)
+            sync()
+            t0 = time.perf_counter()
+            go(acts2, False)
+            sync()
+            wall2 = time.perf_counter() - t0
+            acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20 + steps2)
+            sync()
+            k2 = go(acts2, True) / 1e3 / launches
+            fused2 = bool(L0.bb_rollout_fused(n2)) and K2 > 0
+            if fused2:
+                b2 = W2 * (K2 * L0.bb_rollout_bytes_per_world_step(n2) + L0.bb_rollout_state_bytes_per_world(n2))
+            else:
+                b2 = L0.bb_algorithmic_bytes_per_world(n2) * W2 * (K2 or 1)
+            key = f"W{W2}_N{n2}" + (f"_R{K2}" if K2 else "")
+            line = {"worlds": W2, "agents": n2, "steps": steps2, "value": W2 * steps2 / wall2, "unit": "env-steps/s",
+                    "ms_per_step": wall2 * 1e3 / steps2,
+                    "kernel": ("bb::k_rollout<%d>" if fused2 else "bb::k_step<%d>") % n2,
+                    "launches_timed": launches, "kernel_avg_us": k2 * 1e6,
+                    "kernel_us_per_step": k2 * 1e6 / (K2 or 1), "achieved": b2 / k2 / 1e9,
+                    "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(key),
+                    "algorithmic_bytes_per_launch": b2}
+            if K2:
+                line["rollout"] = K2
+            del sim2, acts2, bufs2
+            torch.cuda.empty_cache()
+            return line
+
+        extra["roofline_beyond_cache"] = config_line(262144, 2)
+        extra["config_c2_8192x2"] = config_line(8192, 2)
+        extra["config_c2_8192x2_rollout32"] = config_line(8192, 2, 32, launches=EVENT_MIN_LAUNCHES // 4)
+        extra["config_c4_shard_32768x2"] = config_line(32768, 2)
+        extra["config_2v2_65536x4"] = config_line(65536, 4)
+        extra["config_c5_65536x10"] = config_line(65536, 10)
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
@@ -370,8 +418,7 @@ def main():
         out["roofline"] = None  # several kernels per step: see the rocprof summary
     if e2e is not None:
         out["e2e"] = e2e
-    if beyond is not None:
-        out["roofline_beyond_cache"] = beyond
+    out.update(extra)
     if rank == 0:
         out["cpu_baseline"] = cpu
         out["cpu_executor"] = cpu_exec

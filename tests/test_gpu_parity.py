@@ -213,3 +213,24 @@ def test_gpu_full_size_sampled_worlds_vs_oracle():
                 assert np.allclose(a, b, atol=1e-5, rtol=1e-6), (w, n)
             else:
                 assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), (w, n)
+
+
+@pytest.mark.parametrize("agents,W", [(2, 65536), (4, 8192)])
+def test_gpu_sharded_worlds_concatenate_to_the_unsharded_run(agents, W):
+    """The multi-GPU partition of SURVEY 8(e) on the HIP path: two simulators
+    owning worlds [0, W/2) and [W/2, W) (world_offset 0 and W/2, the C4 shard
+    of 32 768 worlds at 2 agents) step their worlds exactly as one W-world
+    simulator does -- every column, bit for bit, after 300 random steps."""
+    steps, half = 300, W // 2
+    full = make_sim(ExecMode.CUDA, W, num_agents=agents, per_world_rng=True)
+    shards = [make_sim(ExecMode.CUDA, half, num_agents=agents, per_world_rng=True, world_offset=r * half)
+              for r in range(2)]
+    full.step_n(steps, random_actions=True, action_seed=321, step0=0)
+    for sh in shards:
+        sh.step_n(steps, random_actions=True, action_seed=321, step0=0)
+    torch.cuda.synchronize()
+    for n in ALL_COLUMNS:
+        cat = torch.cat([sh._views[n] for sh in shards], dim=0)
+        assert torch.equal(cat.view(torch.int32), full._views[n].view(torch.int32)), n
+    # and the game actually happened on both shards
+    assert int(full._views["rng_counter"][:half].sum()) > 0 and int(full._views["rng_counter"][half:].sum()) > 0
