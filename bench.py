@@ -202,17 +202,25 @@ def main():
     if K:
         if args.steps % K:
             raise SystemExit("--steps must be a multiple of --rollout")
-        bufs = sim.rollout_buffers(K)  # reused by every chunk, like PPO's storage between updates
+        bufs = None if args.policy else sim.rollout_buffers(K)  # reused by every chunk, like PPO's storage
 
     if args.policy:
         from madrona_basketball_amd.policy import FusedPolicy, make_agent
         pol = FusedPolicy.from_agent(make_agent(0).to(dev))
         lp = torch.empty((W,), dtype=torch.float32, device=dev)
         val = torch.empty((W,), dtype=torch.float32, device=dev)
+        if K:  # PPO's rollout storage (scripts/buffers.py), reused by every chunk
+            pbufs = pol.rollout_buffers(sim, K)
 
     def run(actions, time_kernels=False, steps=None):
         """All staged steps: one step per launch, or chunks of K via bb_rollout."""
         steps = args.steps if steps is None else steps
+        if args.policy and K:  # PPO's rollout on the device (bb_rollout_policy), K steps per call
+            ms = 0.0
+            for i in range(0, steps, K):
+                ms += pol.rollout(sim, K, pbufs, trainee=0, stochastic=True, seed=args.seed, step0=i,
+                                  time_kernels=time_kernels) or 0.0
+            return ms
         if args.policy:  # actions come from the policy, not the staged rows
             for t in range(steps):
                 for a in range(args.agents):
@@ -244,8 +252,8 @@ def main():
     # least EVENT_MIN_LAUNCHES launches whatever --steps is, so the line's
     # frac is an average as long as the committed rocprof summaries'
     del staged
-    if on_gpu and not args.policy:
-        per_launch = K if (K and fused) else 1
+    if on_gpu and (not args.policy or K):
+        per_launch = K if (K and (fused or args.policy)) else 1
         ev_steps = max(args.steps, EVENT_MIN_LAUNCHES * per_launch)
         if K:
             ev_steps = (ev_steps + K - 1) // K * K
@@ -350,12 +358,44 @@ def main():
             torch.cuda.empty_cache()
             return line
 
+        def ppo_line(W2, K2=32, rollouts=10):
+            """PPO's rollout loop on the device (bb_rollout_policy): K2 x (policy on
+            agent 0's rows, step, buffer stores) + the next-value pass."""
+            from madrona_basketball_amd.policy import FusedPolicy, make_agent
+            sim2 = mba.SimpleGridworldSimulator(
+                discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
+                max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W2, gpu_id=dev.index,
+                num_agents=2, per_world_rng=True)
+            pol2 = FusedPolicy.from_agent(make_agent(0).to(dev))
+            b2 = pol2.rollout_buffers(sim2, K2)
+            for i in range(2):
+                pol2.rollout(sim2, K2, b2, seed=args.seed, step0=i * K2)
+            sync()
+            t0 = time.perf_counter()
+            for i in range(rollouts):
+                pol2.rollout(sim2, K2, b2, seed=args.seed, step0=(2 + i) * K2)
+            sync()
+            wall2 = time.perf_counter() - t0
+            ev = sum(pol2.rollout(sim2, K2, b2, seed=args.seed, step0=(2 + rollouts + i) * K2, time_kernels=True)
+                     for i in range(rollouts)) / rollouts
+            line = {"worlds": W2, "agents": 2, "rollout": K2, "rollouts": rollouts,
+                    "value": W2 * K2 * rollouts / wall2, "unit": "env-steps/s",
+                    "us_per_step": wall2 * 1e6 / (K2 * rollouts), "rollout_avg_us_events": ev * 1e3,
+                    "what": "bb_rollout_policy: per step the fused policy acts for agent 0 of every world, the "
+                            "step, obs/actions/log-probs/values/rewards/dones recorded ([K, W, ...]); then the "
+                            "next-value pass (scripts/ppo.py:61-141)"}
+            del sim2, pol2, b2
+            torch.cuda.empty_cache()
+            return line
+
         extra["roofline_beyond_cache"] = config_line(262144, 2)
         extra["config_c2_8192x2"] = config_line(8192, 2)
         extra["config_c2_8192x2_rollout32"] = config_line(8192, 2, 32, launches=EVENT_MIN_LAUNCHES // 4)
         extra["config_c4_shard_32768x2"] = config_line(32768, 2)
         extra["config_2v2_65536x4"] = config_line(65536, 4)
         extra["config_c5_65536x10"] = config_line(65536, 10)
+        extra["ppo_rollout32_8192x2"] = ppo_line(8192)
+        extra["ppo_rollout32_65536x2"] = ppo_line(65536)
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
@@ -391,9 +431,14 @@ def main():
                            f"{L.bb_obs_width(args.agents)} floats") + "), threefry random actions per step (buckets "
                         f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
                         + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
-                           f"of every step recorded into [{K}, W, N, ...] buffers" if K else "; one step per call")
-                        + ("; actions from the fused policy (reference Agent layout, random init, Gumbel "
-                           "sampling) for every agent before each step" if args.policy else ""),
+                           f"of every step recorded into [{K}, W, N, ...] buffers" if K and not args.policy
+                           else ("" if K else "; one step per call"))
+                        + ((f"; PPO's rollout on the device (bb_rollout_policy: per step the fused policy "
+                            f"-- reference Agent layout, random init, Gumbel sampling -- acts for agent 0, the "
+                            f"step, and obs/actions/log-probs/values/rewards/dones recorded into [{K}, W, ...] "
+                            f"buffers; agent 1 by the in-sim defence AI; the staged random rows are unused)"
+                            if K else "; actions from the fused policy (reference Agent layout, random init, "
+                            "Gumbel sampling) for every agent before each step") if args.policy else ""),
             "worlds_per_gpu": W,
             "total_worlds": total_worlds,
             "agents_per_world": args.agents,
@@ -416,6 +461,11 @@ def main():
         out["config"]["parallelism"] += " (host executor, gloo)"
     if args.policy:
         out["roofline"] = None  # several kernels per step: see the rocprof summary
+        if K and on_gpu:
+            out["policy_rollout"] = {"rollout_avg_us": avg_kernel_s * 1e6, "us_per_step": avg_kernel_s * 1e6 / K,
+                                     "rollouts_timed": launches,
+                                     "timing": "events around each bb_rollout_policy call (its K policy passes, "
+                                               "K steps and the next-value pass)"}
     if e2e is not None:
         out["e2e"] = e2e
     out.update(extra)

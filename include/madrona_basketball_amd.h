@@ -24,6 +24,8 @@
  *   bb_policy_forward   <- Agent.forward of scripts/agent.py:140-154 (32 channels,
  *                          2 layers, env.py:107) + the action write of
  *                          scripts/env.py:147, fused on the device
+ *   bb_rollout_policy   <- rollout() of scripts/ppo.py:61-141: n x (agent(obs);
+ *                          env.step; buffer stores) + agent.evaluate(obs_)
  *   bb_set_action       <- Manager::setAction          src/mgr.cpp:270-293
  *   bb_trigger_reset    <- Manager::triggerReset       src/mgr.cpp:297-311
  *   bb_export           <- Manager::*Tensor() getters  src/mgr.cpp:317-445
@@ -222,6 +224,31 @@ typedef struct bb_policy_weights {
 int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu_id, const float *obs,
                       int64_t rows, int64_t obs_stride, int32_t *actions, int64_t action_stride, float *log_prob,
                       float *value, int32_t stochastic, uint32_t seed, uint32_t step, void *stream);
+
+/* PPO's rollout on the device (scripts/ppo.py:61-141 over scripts/env.py:126-170;
+ * the reference's 2-agent game).  For k = 0..n-1:
+ *     actions, log_probs, values = agent(obs)          (policy w, trainee rows)
+ *     [opponent: the frozen policy acts for the other agent, env.py:127-143]
+ *     actions[:, trainee] = actions; bb_step()          (env.py:147,155)
+ *     buffer.obs/actions/log_probs/values[k] = obs, actions, log_probs, values
+ *     buffer.rewards/dones[k] = the trainee's reward / done after the step
+ * and then next_value = agent.evaluate(obs after the last step) (ppo.py:136-137).
+ * Each output is optional (NULL: not recorded; reward and done together).
+ * Layouts (the simulator's device, host memory in CPU mode): obs float [n][W][128],
+ * actions int32 [n][W][6] (the policy's, before the defence AI's overrides),
+ * log_prob / value / reward / done float [n][W], next_value float [W].
+ * Sampling as bb_policy_forward with step = step0 + k (stochastic = 0: argmax);
+ * the opponent samples with seed ^ 0x9E3779B9.  Equal, bit for bit, to n x
+ * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
+ * kernel_ms (CUDA mode): time from the first launch to the last, after a sync. */
+typedef struct bb_policy_rollout_buffers {
+    float *obs;
+    int32_t *actions;
+    float *log_prob, *value, *reward, *done, *next_value;
+} bb_policy_rollout_buffers;
+int bb_rollout_policy(bb_sim *sim, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
+                      int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
+                      const bb_policy_rollout_buffers *out, void *stream, float *kernel_ms);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

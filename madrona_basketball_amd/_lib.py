@@ -42,7 +42,7 @@ ABI_SYMBOLS = [
     "bb_default_config", "bb_obs_width", "bb_buffer_bytes", "bb_create",
     "bb_create_with_buffers", "bb_destroy", "bb_step", "bb_step_n",
     "bb_write_random_actions", "bb_step_n_staged", "bb_fill_random_actions", "bb_rollout",
-    "bb_record_words", "bb_record", "bb_policy_forward",
+    "bb_record_words", "bb_record", "bb_policy_forward", "bb_rollout_policy",
     "bb_set_action", "bb_trigger_reset", "bb_export",
     "bb_num_worlds", "bb_num_agents", "bb_exec_mode", "bb_algorithmic_bytes_per_world",
     "bb_rollout_fused", "bb_rollout_bytes_per_world_step", "bb_rollout_state_bytes_per_world",
@@ -65,6 +65,11 @@ class Config(ctypes.Structure):
 class PolicyWeights(ctypes.Structure):
     _fields_ = [(n, ctypes.c_void_p) for n in ("obs_mean", "obs_inv", "w1", "b1", "ln1_w", "ln1_b", "w2", "b2",
                                                "ln2_w", "ln2_b", "head_w", "head_b")]
+
+
+class PolicyRolloutBuffers(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("obs", "actions", "log_prob", "value", "reward", "done",
+                                               "next_value")]
 
 
 _lib = None
@@ -105,6 +110,9 @@ def load():
         "bb_policy_forward": (ctypes.c_int, [ctypes.POINTER(PolicyWeights), i32, i32, vp, i64, i64, vp, i64, vp, vp,
                                              i32, u32, u32, vp]),
         "bb_record": (ctypes.c_int, [vp, i64, i32, vp, i64, vp]),
+        "bb_rollout_policy": (ctypes.c_int, [vp, ctypes.POINTER(PolicyWeights), ctypes.POINTER(PolicyWeights), i32,
+                                             i32, i32, u32, u32, ctypes.POINTER(PolicyRolloutBuffers), vp,
+                                             ctypes.POINTER(ctypes.c_float)]),
         "bb_set_action": (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "bb_trigger_reset": (ctypes.c_int, [vp, i32, vp]),
         "bb_export": (ctypes.c_int, [vp, i32, ctypes.POINTER(vp), ctypes.POINTER(i32),

@@ -774,7 +774,7 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
         if (!ptr) return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: a weight pointer is NULL");
     if ((((uintptr_t)obs) & 15u) || (obs_stride & 3) || (((uintptr_t)w->w1) & 15u))
         return fail(BB_ERR_INVALID_ARG, "bb_policy_forward: obs rows and w1 must be 16-byte aligned");
-    bb::PolicyArgs a;
+    bb::PolicyArgs a{};
     a.w = bb::PolicyWeights{w->obs_mean, w->obs_inv, w->w1, w->b1, w->ln1_w, w->ln1_b,
                             w->w2, w->b2, w->ln2_w, w->ln2_b, w->head_w, w->head_b};
     a.obs = obs; a.obs_stride = obs_stride; a.rows = rows;
@@ -789,6 +789,122 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
     DeviceGuard g(gpu_id);
     hipError_t e = bb::launch_policy(a, (hipStream_t)stream);
     if (e != hipSuccess) return hip_fail(e, "launch policy kernel");
+    return BB_OK;
+}
+
+namespace {
+
+bool weights_ok(const bb_policy_weights *w)
+{
+    if (!w) return false;
+    const float *req[] = {w->obs_mean, w->obs_inv, w->w1, w->b1, w->ln1_w, w->ln1_b, w->w2, w->b2, w->ln2_w,
+                          w->ln2_b, w->head_w, w->head_b};
+    for (const float *ptr : req)
+        if (!ptr) return false;
+    return (((uintptr_t)w->w1) & 15u) == 0;
+}
+
+bb::PolicyWeights policy_weights(const bb_policy_weights *w)
+{
+    return bb::PolicyWeights{w->obs_mean, w->obs_inv, w->w1, w->b1, w->ln1_w, w->ln1_b,
+                             w->w2, w->b2, w->ln2_w, w->ln2_b, w->head_w, w->head_b};
+}
+
+}  // namespace
+
+int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
+                      int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
+                      const bb_policy_rollout_buffers *out, void *stream, float *kernel_ms)
+{
+    if (!s || n < 0 || !out) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: arguments");
+    if (kernel_ms) *kernel_ms = 0.f;
+    if (!weights_ok(w) || (opponent && !weights_ok(opponent)))
+        return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: a weight pointer is NULL or w1 is not 16-byte aligned");
+    if (s->n != 2) return fail(BB_ERR_UNSUPPORTED, "bb_rollout_policy: the reference's 2-agent game only");
+    if (trainee < 0 || trainee >= s->n) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: trainee index");
+    if (n == 0) return BB_OK;
+    if ((out->reward == nullptr) != (out->done == nullptr))
+        return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: reward and done are recorded together");
+    const int64_t W = s->cfg.num_worlds, N = s->n, ow = bb::obs_width(s->n);
+    const bb::Columns &c = s->p.c;
+    // Per step k (scripts/ppo.py:65-134 over scripts/env.py:126-170):
+    //   actions, log_probs, values = agent(obs)       policy on the trainee rows
+    //   [frozen opponent acts, env.py:127-143]        policy on the other rows
+    //   actions[:, trainee] = a; worlds.step()         env.py:147,155
+    //   buffer.{obs, actions, log_probs, values}[k]    recorded by the policy pass
+    //   buffer.{rewards, not_dones}[k]                 recorded by the next pass
+    // and after the last step next_value = agent.evaluate(obs_) (ppo.py:136-137),
+    // a value-only pass that also records step n-1's rewards / dones.
+    auto pass = [&](int32_t k, bool final_pass) {
+        bb::PolicyArgs a{};
+        a.w = policy_weights(w);
+        a.obs = c.obs + trainee * ow; a.obs_stride = N * ow; a.rows = W;
+        a.stochastic = stochastic ? 1 : 0; a.seed = seed; a.step = step0 + (uint32_t)k;
+        if (!final_pass) {
+            a.actions = c.action + trainee * 6; a.act_stride = N * 6;
+            a.obs_out = out->obs ? out->obs + (int64_t)k * W * bb::POL_IN : nullptr;
+            a.act_out = out->actions ? out->actions + (int64_t)k * W * 6 : nullptr;
+            a.log_prob = out->log_prob ? out->log_prob + (int64_t)k * W : nullptr;
+            a.value = out->value ? out->value + (int64_t)k * W : nullptr;
+        } else {
+            a.value = out->next_value;
+        }
+        if (k > 0 && out->reward) {
+            a.rew_src = c.reward + trainee; a.done_src = c.done + trainee; a.rd_stride = N;
+            a.rew_out = out->reward + (int64_t)(k - 1) * W;
+            a.done_out = out->done + (int64_t)(k - 1) * W;
+        }
+        return a;
+    };
+    auto opp_pass = [&](int32_t k) {
+        bb::PolicyArgs a{};
+        a.w = policy_weights(opponent);
+        const int other = 1 - trainee;
+        a.obs = c.obs + other * ow; a.obs_stride = N * ow; a.rows = W;
+        a.actions = c.action + other * 6; a.act_stride = N * 6;
+        // the frozen policy samples (Agent.forward's default) with its own key
+        a.stochastic = 1; a.seed = seed ^ 0x9E3779B9u; a.step = step0 + (uint32_t)k;
+        return a;
+    };
+    const bool final_needed = out->next_value != nullptr || out->reward != nullptr;
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) {
+        for (int32_t k = 0; k < n; k++) {
+            bb::host_policy(pass(k, false));
+            if (opponent) bb::host_policy(opp_pass(k));
+            int rc = bb::host_step(s->n, s->p, *s->pool);
+            if (rc != BB_OK) return rc;
+        }
+        if (final_needed) bb::host_policy(pass(n, true));
+        return BB_OK;
+    }
+    DeviceGuard g(s->device);
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (kernel_ms) {
+        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
+            return fail(BB_ERR_HIP, "hipEventCreate");
+        (void)hipEventRecord(e0, st);
+    }
+    for (int32_t k = 0; k < n; k++) {
+        hipError_t e = bb::launch_policy(pass(k, false), st);
+        if (e == hipSuccess && opponent) e = bb::launch_policy(opp_pass(k), st);
+        if (e == hipSuccess) e = bb::launch_step(s->n, s->p, st);
+        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
+    }
+    if (final_needed) {
+        hipError_t e = bb::launch_policy(pass(n, true), st);
+        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
+    }
+    if (kernel_ms) {
+        (void)hipEventRecord(e1, st);
+        hipError_t e = hipEventSynchronize(e1);
+        float ms = 0.f;
+        if (e == hipSuccess) (void)hipEventElapsedTime(&ms, e0, e1);
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+        *kernel_ms = ms;
+    }
     return BB_OK;
 }
 

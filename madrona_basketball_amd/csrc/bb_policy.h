@@ -46,6 +46,13 @@ struct PolicyArgs {
     float *value;          // [rows] (optional)
     int32_t stochastic;    // 0: argmax (best), 1: Gumbel-max sample
     uint32_t seed, step;   // sample key: threefry({seed, step}, {row, logit})
+    // actions == nullptr: no actions written (value only, agent.evaluate).
+    // Rollout recording (bb_rollout_policy, scripts/ppo.py:129-134; all optional):
+    float *obs_out;                   // row r's 128 observation floats -> obs_out + r * 128
+    int32_t *act_out;                 // row r's 6 actions -> act_out + r * 6
+    const float *rew_src, *done_src;  // the previous step's reward / done of row r at src + r * rd_stride
+    int64_t rd_stride;
+    float *rew_out, *done_out;        // -> rew_out[r], done_out[r]
 };
 
 // exp / log in f32 from a fixed sequence of f32 operations (identical bits on
@@ -201,10 +208,20 @@ inline void policy_row_host(const PolicyArgs &a, int64_t r)
     int32_t act[6];
     float lp;
     pol_select(out, a.stochastic != 0, a.seed, a.step, (uint32_t)r, act, &lp);
-    int32_t *d = a.actions + r * a.act_stride;
-    for (int b = 0; b < 6; b++) d[b] = act[b];
+    if (a.obs_out)
+        for (int k = 0; k < POL_IN; k++) a.obs_out[r * POL_IN + k] = o[k];
+    if (a.actions) {
+        int32_t *d = a.actions + r * a.act_stride;
+        for (int b = 0; b < 6; b++) d[b] = act[b];
+    }
+    if (a.act_out)
+        for (int b = 0; b < 6; b++) a.act_out[r * 6 + b] = act[b];
     if (a.log_prob) a.log_prob[r] = lp;
     if (a.value) a.value[r] = out[POL_LOGITS];
+    if (a.rew_out) {
+        a.rew_out[r] = a.rew_src[r * a.rd_stride];
+        a.done_out[r] = a.done_src[r * a.rd_stride];
+    }
 }
 
 }  // namespace bb

@@ -111,6 +111,12 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
                     const float4 o = src[v];
                     x[m][4 * v] = o.x; x[m][4 * v + 1] = o.y; x[m][4 * v + 2] = o.z; x[m][4 * v + 3] = o.w;
                 }
+                if (a.obs_out) {  // the rollout's record of the observed row (buffer.obs, ppo.py:129)
+                    float4 *dst = (float4 *)(a.obs_out + r * POL_IN + 32 * q);
+#pragma unroll
+                    for (int v = 0; v < 8; v++)
+                        dst[v] = make_float4(x[m][4 * v], x[m][4 * v + 1], x[m][4 * v + 2], x[m][4 * v + 3]);
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < 32; j++) x[m][j] = 0.f;
@@ -184,11 +190,23 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
             int32_t act[6];
             float lp;
             pol_select(logit, a.stochastic != 0, a.seed, a.step, (uint32_t)rr, act, &lp);
-            int32_t *d = a.actions + rr * a.act_stride;
+            if (a.actions) {
+                int32_t *d = a.actions + rr * a.act_stride;
 #pragma unroll
-            for (int b = 0; b < 6; b++) d[b] = act[b];
+                for (int b = 0; b < 6; b++) d[b] = act[b];
+            }
+            if (a.act_out) {
+                int2 *d = (int2 *)(a.act_out + rr * 6);
+                d[0] = make_int2(act[0], act[1]);
+                d[1] = make_int2(act[2], act[3]);
+                d[2] = make_int2(act[4], act[5]);
+            }
             if (a.log_prob) a.log_prob[rr] = lp;
             if (a.value) a.value[rr] = logit[POL_LOGITS];
+            if (a.rew_out) {  // the previous step's outcome of this row (buffer.rewards / not_dones)
+                a.rew_out[rr] = a.rew_src[rr * a.rd_stride];
+                a.done_out[rr] = a.done_src[rr * a.rd_stride];
+            }
         }
         __syncthreads();
     }

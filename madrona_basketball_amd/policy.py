@@ -173,3 +173,55 @@ class FusedPolicy:
         obs = sim.observations_tensor().to_torch()[:, agent_idx]
         act = sim.action_tensor().to_torch()[:, agent_idx]
         self.forward_into(obs, act, log_prob, value, stochastic, seed, step)
+
+    # ------------------------------------------------------------ PPO rollout
+    ROLLOUT_KEYS = ("obs", "actions", "log_prob", "value", "reward", "done", "next_value")
+
+    def rollout_buffers(self, sim, n: int) -> dict:
+        """Zeroed outputs of rollout() on the simulator's device -- the storage of
+        scripts/buffers.py:4-11 for n steps of the trainee (obs [n, W, 128],
+        actions int32 [n, W, 6], log_prob / value / reward / done [n, W]) and
+        next_value [W] (ppo.py:136-137)."""
+        W, dev, f32 = sim.num_worlds, sim.device, torch.float32
+        return {"obs": torch.zeros((n, W, IN), dtype=f32, device=dev),
+                "actions": torch.zeros((n, W, 6), dtype=torch.int32, device=dev),
+                "log_prob": torch.zeros((n, W), dtype=f32, device=dev),
+                "value": torch.zeros((n, W), dtype=f32, device=dev),
+                "reward": torch.zeros((n, W), dtype=f32, device=dev),
+                "done": torch.zeros((n, W), dtype=f32, device=dev),
+                "next_value": torch.zeros((W,), dtype=f32, device=dev)}
+
+    def rollout(self, sim, n: int, buffers: dict, trainee: int = 0, stochastic: bool = True, seed: int = 0,
+                step0: int = 0, opponent: "FusedPolicy" = None, time_kernels: bool = False):
+        """PPO's rollout loop (scripts/ppo.py:61-141) on the device, bb_rollout_policy:
+        n x (this policy acts for agent `trainee` of every world; [the frozen
+        `opponent` acts for the other agent, env.py:127-143]; step) with the
+        buffer stores of ppo.py:129-134 and next_value = evaluate(last obs).
+        Bit for bit n x (act(); [opponent.act()]; sim.step()) with the same reads.
+        Any entry of `buffers` may be None (not recorded).  Returns the elapsed
+        device ms when time_kernels."""
+        W = sim.num_worlds
+        shapes = {"obs": ((n, W, IN), torch.float32), "actions": ((n, W, 6), torch.int32),
+                  "log_prob": ((n, W), torch.float32), "value": ((n, W), torch.float32),
+                  "reward": ((n, W), torch.float32), "done": ((n, W), torch.float32),
+                  "next_value": ((W,), torch.float32)}
+        ptrs = {}
+        for k in self.ROLLOUT_KEYS:
+            t = buffers.get(k)
+            if t is not None:
+                shp, dt = shapes[k]
+                if tuple(t.shape) != shp or t.dtype != dt or not t.is_contiguous() or t.device != sim.device:
+                    raise ValueError(f"rollout buffer {k!r} must be a contiguous {dt} {shp} tensor on the "
+                                     "simulator's device")
+            ptrs[k] = None if t is None else t.data_ptr()
+        if (buffers.get("reward") is None) != (buffers.get("done") is None):
+            raise ValueError("reward and done are recorded together")
+        if sim.device != self.device or (opponent is not None and opponent.device != self.device):
+            raise ValueError("policy, opponent and simulator must share a device")
+        out = _lib.PolicyRolloutBuffers(**ptrs)
+        ms = ctypes.c_float(0.0)
+        _lib.check(_lib.load().bb_rollout_policy(
+            sim._h, ctypes.byref(self._w), ctypes.byref(opponent._w) if opponent is not None else None, int(n),
+            int(trainee), 1 if stochastic else 0, int(seed) & 0xFFFFFFFF, int(step0) & 0xFFFFFFFF,
+            ctypes.byref(out), sim._stream(), ctypes.byref(ms) if time_kernels else None), "rollout_policy")
+        return ms.value if time_kernels else None
