@@ -1066,6 +1066,34 @@ int bb_diag_math(int32_t fn, const float *x, const float *y, float *out, int64_t
     return BB_OK;
 }
 
+// Diagnostic (not in the public header): one k_policy launch over `rows`
+// rows with per-wave phase clocks (bb_policy.hip pol_trace) copied to
+// out[waves][POL_TRACE_POINTS]; *waves = the launch's waves.
+int bb_diag_policy_trace(const bb_policy_weights *w, int32_t gpu_id, const float *obs, int64_t rows,
+                         int64_t obs_stride, int32_t stochastic, void *stream, uint64_t *out, int64_t max_waves,
+                         int64_t *waves)
+{
+    if (!weights_ok(w) || !obs || rows <= 0 || !out || !waves) return fail(BB_ERR_INVALID_ARG, "bb_diag_policy_trace");
+    DeviceGuard g(gpu_id);
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t cap = 1 << 16;
+    bb::PolicyArgs a{};
+    a.w = policy_weights(w);
+    a.obs = obs; a.obs_stride = obs_stride; a.rows = rows;
+    a.stochastic = stochastic ? 1 : 0; a.seed = 1; a.step = 2;
+    if (hipMalloc(&a.diag_ts, (size_t)cap * bb::POL_TRACE_POINTS * 8) != hipSuccess) return fail(BB_ERR_OOM, "trace");
+    (void)hipMemsetAsync(a.diag_ts, 0, (size_t)cap * bb::POL_TRACE_POINTS * 8, st);
+    hipError_t e = bb::launch_policy(a, st);
+    if (e == hipSuccess) e = bb::launch_policy(a, st);
+    const int64_t n = max_waves < cap ? max_waves : cap;
+    if (e == hipSuccess) e = hipMemcpyAsync(out, a.diag_ts, (size_t)n * bb::POL_TRACE_POINTS * 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(a.diag_ts);
+    if (e != hipSuccess) return hip_fail(e, "policy trace");
+    *waves = n;
+    return BB_OK;
+}
+
 int64_t bb_algorithmic_bytes_per_world(int32_t n)
 {
     // B(N) = N (268 + 4 obs_used(N)) + 152

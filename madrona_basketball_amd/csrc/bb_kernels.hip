@@ -434,12 +434,12 @@ __device__ __forceinline__ X unpark_words(const float *tile, int lane)
 // the lane's intrinsic block, exchanged with the world's lanes by DPP, then
 // the row through the LDS tile (fast rows) or directly (slow rows).
 // ib / share: inbounder_id and obs_sharable of the world in creation order.
-template <int N, int MODE, class T = PhasedTile<N>>
-__device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
-                                               int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
+// The row sources of the lane's agent (slot 0 of its view v): the intrinsic
+// blocks of every agent of the world (its own computed here, the others' by
+// DPP from their lanes) and the directions / distances to the others.
+template <int N>
+__device__ __forceinline__ void lane_shared_obs(const World<N> &v, const Ctx &c, bool active, SharedObs<N> &sh)
 {
-    constexpr int OW = obs_width(N);
-    SharedObs<N> sh;
     if (active) {
         Intrinsic mine, slot[N];
         {
@@ -463,6 +463,15 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
             sh.rlen[0][t] = bbm::sqrtf_(l2);
         }
     }
+}
+
+template <int N, int MODE, class T = PhasedTile<N>>
+__device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
+                                               int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
+{
+    constexpr int OW = obs_width(N);
+    SharedObs<N> sh;
+    lane_shared_obs(v, c, active, sh);
     float *grow = obs + (w * N + k) * (int64_t)OW;
     const bool fast = active && canonical_slots(v, 0);
     if constexpr (MODE == MODE_DIRECT_OBS) {
@@ -538,6 +547,205 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     const bool share = active && obs_sharable(s);
     agent_lane_obs<N, MODE, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
     trace_point<MODE>(p, 9);
+}
+
+// ------------------------------------------------------------------ wide step
+// Small world counts (C2, the reference's 8 192-world training batch: 256
+// waves of k_step = one per CU, 3 of every 4 SIMDs idle) leave k_step's time
+// to one wave's dependent chain.  k_step_wide gives each 32-world group a
+// workgroup of WIDE_WAVES waves on different SIMDs; all load the same worlds
+// and run the shared part of the chain (every system whose result another
+// system reads) redundantly -- free in latency, on otherwise idle SIMDs --
+// and split what only the outputs need:
+//   PCT    systems 1-8 only: the shot percentage (erf / atan, the longest
+//          per-agent tail) runs beside the others' systems 9-16 and reaches
+//          them through LDS (nothing in systems 9-17 reads it; a reset
+//          zeroes it, which the others see as their own reset);
+//   DEF    hardCodeDefense, then the Action and Attributes columns;
+//   STORE  reward, then every other state column (and the event-only words);
+//   OBS p  pass p of the observation rows (PhasedTile windows).
+// Every wave stores or emits a disjoint set of words, bit-identical to
+// k_step's (the same system code runs on the same inputs).
+constexpr int WIDE_DEF = 0, WIDE_PCT = 1, WIDE_STORE = 2, WIDE_OBS0 = 3;
+template <int N>
+struct Wide {
+    using T = StepTile<N, false>;
+    static constexpr int OBS_WAVES = T::PH;
+    static constexpr int WAVES = WIDE_OBS0 + OBS_WAVES;
+    static constexpr int TILES = 1 + OBS_WAVES;  // STORE's parked words, one tile per OBS wave
+    static constexpr int FLOATS = TILES * T::FLOATS + 2 * ERF_WORDS + WAVE;
+};
+#ifndef BB_WIDE_MAX_WAVES
+#define BB_WIDE_MAX_WAVES 0  // k_step_wide while k_step would have at most this many waves (0: never; A/B in DESIGN.md)
+#endif
+constexpr uint32_t SHOT_PCT_UNSET = 0x7FC0BEEFu;  // a NaN the step never computes
+
+// Ordering of LDS words written and read by different lanes of one wave (a
+// wave's LDS operations execute in order): keeps the compiler from moving
+// them across each other.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int N, int PHASE>
+__device__ __forceinline__ void wide_obs_pass(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,
+                                              int64_t w0, int64_t w, bool active, float *tile, float *obs)
+{
+    using T = typename Wide<N>::T;
+    SharedObs<N> sh;
+    lane_shared_obs(v, c, active, sh);
+    const bool fast = active && canonical_slots(v, 0);
+    // rows the tile does not carry are written whole by the first pass's wave
+    if (PHASE == 0 && active && !fast) fill_obs_slow(v, c, 0, obs + (w * N + k) * (int64_t)obs_width(N), ib);
+    if (fast) emit_phase<N, T, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
+    wave_sync();
+    constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
+    constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, w0 * N, __ballot(fast), lane);
+}
+
+template <int N, int OP = 0>
+__device__ __forceinline__ void wide_obs_dispatch(int op, const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
+                                                  int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
+{
+    if constexpr (OP < Wide<N>::OBS_WAVES) {
+        if (op == OP) wide_obs_pass<N, OP>(v, c, ib, share, k, lane, w0, w, active, tile, obs);
+        else wide_obs_dispatch<N, OP + 1>(op, v, c, ib, share, k, lane, w0, w, active, tile, obs);
+    }
+}
+
+// MODE_TRACE: lane 0 of each wave records the clock at 0 start, 1 state
+// loaded, 2 after the first barrier, 3 systems done, 4 after the second
+// barrier, 9 end, into diag_ts[(workgroup * WAVES + wave) * TRACE_POINTS].
+template <int N, int MODE>
+__device__ __forceinline__ void wide_trace(const Params &p, int wave, int point)
+{
+    if constexpr (MODE == MODE_TRACE) {
+        if (point == 1) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = wall_clock64();
+        if (threadIdx.x % WAVE == 0)
+            p.diag_ts[((int64_t)blockIdx.x * Wide<N>::WAVES + wave) * TRACE_POINTS + point] = t;
+    }
+}
+
+template <int N, int MODE = MODE_FULL>
+__device__ __forceinline__ void step_agent_lanes_wide(const Params &p, float *lds)
+{
+    using T = typename Wide<N>::T;
+    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+    const int lane = (int)threadIdx.x % WAVE;
+    const int k = lane % N;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
+    const LaneAgents<N, MODE_FULL> ag{k, &p};
+    // LDS: [STORE parked words | OBS tiles][erf table (PCT)][shot percentages]
+    float *tile = lds + (wave >= WIDE_STORE ? (wave - WIDE_STORE) * T::FLOATS : 0);
+    double *erf_tab = (double *)(lds + Wide<N>::TILES * T::FLOATS);
+    float *pct = lds + Wide<N>::TILES * T::FLOATS + 2 * ERF_WORDS;
+
+    World<N> s;
+    // memory side effects of the systems (Stats, Team in score / reset) from
+    // one wave only
+    Ctx c = make_ctx(p, w, k == 0 && wave == WIDE_STORE);
+    wide_trace<N, MODE>(p, wave, 0);
+    if (wave == WIDE_PCT) {
+        // the erf table into LDS (its loads issued before the state's)
+        double e[(ERF_WORDS + WAVE - 1) / WAVE];
+#pragma unroll
+        for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
+            const int i = j * WAVE + lane;
+            e[j] = i < ERF_WORDS ? (&bbm::ERF_TAYLOR[0][0])[i] : 0.0;
+        }
+        if (active) load_world(s, p, w);
+#pragma unroll
+        for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
+            const int i = j * WAVE + lane;
+            if (i < ERF_WORDS) erf_tab[i] = e[j];
+        }
+        wave_sync();
+        c.erf_tab = erf_tab;
+    } else if (active) {
+        load_world(s, p, w);
+    }
+    if (wave == WIDE_STORE && active) {
+        Orig<N> o;
+        capture(o, s);
+        LaneOrig x;
+        x.world = world_orig(o);
+        x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
+        park_words(tile, lane, x);
+    }
+    wide_trace<N, MODE>(p, wave, 1);
+    // every wave has loaded the columns before any wave writes one (the
+    // systems' own side effects: Stats, Team)
+    __syncthreads();
+    wide_trace<N, MODE>(p, wave, 2);
+    if (active) {
+        constexpr uint32_t LATE = (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14)
+                                  | (1u << 15) | (1u << 16) | (1u << 17);
+        uint32_t skip;
+        if (wave == WIDE_PCT) {
+            skip = LATE;  // systems 1-8
+        } else {
+            skip = (1u << 8) | (1u << 17);  // all but the shot percentage and the defence
+#pragma unroll
+            for (int i = 0; i < N; i++) s.attr[i][8] = bitsf(SHOT_PCT_UNSET);
+        }
+        step_world_pre_obs(s, c, ag, skip, 0u);
+        if (wave == WIDE_PCT) pct[lane] = pick_by<N>(k, [&](int j) { return s.attr[j][8]; });
+    }
+    wide_trace<N, MODE>(p, wave, 3);
+    __syncthreads();  // the shot percentages are in LDS
+    wide_trace<N, MODE>(p, wave, 4);
+    if (wave == WIDE_PCT) {  // (no workgroup barrier follows)
+        wide_trace<N, MODE>(p, wave, 9);
+        return;
+    }
+    if (active) {
+        // systems 9-17 left attribute 8 alone unless a reset zeroed it
+#pragma unroll
+        for (int i = 0; i < N; i++)
+            if (fbits(s.attr[i][8]) == SHOT_PCT_UNSET) s.attr[i][8] = pct[lane - k + i];
+    }
+    World<N> v;  // the world with this lane's agent in slot 0
+    if (wave == WIDE_DEF) {
+        if (active) {
+            sys_defense(s, c, ag);
+            agent_view(s, v, k);
+            store_world_agent<N, -1, STORE_ACT_ATTR>(v, p, w * N + k, 0);
+        }
+    } else if (wave == WIDE_STORE) {
+        if (active) {
+            agent_view(s, v, k);
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
+            store_world_agent<N, -1, STORE_REST>(v, p, w * N + k, 0, &x.agent);
+            if (k == 0) {
+                Orig<N> o;
+                set_world_orig(o, x.world);
+                store_world_shared(s, p, w, &o);
+            }
+        }
+    } else {
+        if (active) agent_view(s, v, k);
+        const int32_t ib = active ? inbounder_id(s) : -1;
+        const bool share = active && obs_sharable(s);
+        wide_obs_dispatch<N>(wave - WIDE_OBS0, v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+    }
+    wide_trace<N, MODE>(p, wave, 9);
+}
+
+template <int N, int MODE = MODE_FULL>
+__global__ __launch_bounds__(WAVE * Wide<N>::WAVES, 1) void k_step_wide(const Params p)
+{
+    if constexpr (N == 2 && BB_AGENT_LANES && !Lanes<N>::SHARED) {
+        __shared__ float4 lds4[(Wide<N>::FLOATS + 3) / 4];
+        step_agent_lanes_wide<N, MODE>(p, (float *)lds4);
+    }
 }
 
 // Timing experiment (diagnostic build, BB_STEP_BLOCKS > 1): each wave steps
@@ -1313,6 +1521,26 @@ bool step_lines(int64_t num_worlds)
     return Lanes<N>::LPW == N && num_worlds * per_world > LINES_MIN_BYTES;
 }
 
+// k_step_wide (N = 2) while k_step would run at most BB_WIDE_MAX_WAVES waves
+// (MADRONA_BB_WIDE_MAX_WAVES overrides it for A/B timing; 0 disables).
+inline int64_t wide_max_waves()
+{
+    static const int64_t v = [] {
+        const char *e = getenv("MADRONA_BB_WIDE_MAX_WAVES");
+        return (int64_t)(e && *e ? atoll(e) : BB_WIDE_MAX_WAVES);
+    }();
+    return v;
+}
+template <int N>
+bool step_wide(int64_t num_worlds)
+{
+    if constexpr (N == 2 && BB_AGENT_LANES && !Lanes<N>::SHARED && BB_STEP_BLOCKS == 1) {
+        return (num_worlds + Lanes<N>::WPB - 1) / Lanes<N>::WPB <= wide_max_waves();
+    } else {
+        return false;
+    }
+}
+
 template <int N>
 hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
@@ -1324,7 +1552,9 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
     case MODE_FULL:
-        if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid_full, block, 0, s, ev0, ev1, 0, p);
+        if (step_wide<N>(p.num_worlds))
+            hipExtLaunchKernelGGL(k_step_wide<N>, grid, dim3(WAVE * Wide<N>::WAVES), 0, s, ev0, ev1, 0, p);
+        else if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid_full, block, 0, s, ev0, ev1, 0, p);
         else hipExtLaunchKernelGGL(k_step<N, MODE_FULL>, grid_full, block, 0, s, ev0, ev1, 0, p);
         break;
     case MODE_IO: BB_LAUNCH(MODE_IO); break;
@@ -1332,7 +1562,12 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
     case MODE_DIRECT_OBS: BB_LAUNCH(MODE_DIRECT_OBS); break;
     case MODE_NO_OBS: BB_LAUNCH(MODE_NO_OBS); break;
     case MODE_SKIP: BB_LAUNCH(MODE_SKIP); break;
-    case MODE_TRACE: BB_LAUNCH(MODE_TRACE); break;
+    case MODE_TRACE:
+        if (step_wide<N>(p.num_worlds))
+            hipExtLaunchKernelGGL(k_step_wide<N, MODE_TRACE>, grid, dim3(WAVE * Wide<N>::WAVES), 0, s, ev0, ev1, 0, p);
+        else
+            BB_LAUNCH(MODE_TRACE);
+        break;
     default: return hipErrorInvalidValue;
     }
 #undef BB_LAUNCH
@@ -1363,6 +1598,10 @@ template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEve
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
 template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value; }
-template <> int step_grid<BB_N>(int64_t num_worlds) { return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB); }
+template <> int step_grid<BB_N>(int64_t num_worlds)
+{
+    const int g = (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB);
+    return step_wide<BB_N>(num_worlds) ? g * Wide<BB_N>::WAVES : g;  // waves of the MODE_FULL launch
+}
 
 }  // namespace bb

@@ -25,7 +25,7 @@ constexpr int POL_HID = 32;     // num_channels
 constexpr int POL_LOGITS = 19;  // sum of the buckets
 constexpr int POL_HEAD = 32;    // head rows: 19 actor + 1 critic + 12 zero
 constexpr int POL_BUCKETS = 6;
-BB_HD int pol_bucket(int b) { return b == 1 ? 8 : (b == 2 ? 3 : 2); }  // [2, 8, 3, 2, 2, 2]
+BB_HD constexpr int pol_bucket(int b) { return b == 1 ? 8 : (b == 2 ? 3 : 2); }  // [2, 8, 3, 2, 2, 2]
 
 // Device (or host) pointers, fp32, row-major [out][in].
 struct PolicyWeights {
@@ -53,7 +53,9 @@ struct PolicyArgs {
     const float *rew_src, *done_src;  // the previous step's reward / done of row r at src + r * rd_stride
     int64_t rd_stride;
     float *rew_out, *done_out;        // -> rew_out[r], done_out[r]
+    uint64_t *diag_ts;                // diagnostics only: POL_TRACE_POINTS clocks of each wave's first tile
 };
+constexpr int POL_TRACE_POINTS = 8;
 
 // exp / log in f32 from a fixed sequence of f32 operations (identical bits on
 // host and gfx950; ~1 ulp): the policy is compared with torch's fp32 forward
@@ -111,43 +113,66 @@ BB_HD float pol_gumbel(uint32_t seed, uint32_t step, uint32_t row, uint32_t i)
 
 // Bucket sampling / scoring of one row's logits (fully unrolled: the bucket
 // sizes and offsets are compile-time, so logit[] stays in registers).
+// Logit offset of bucket b ([2, 8, 3, 2, 2, 2]).
+BB_HD constexpr int pol_bucket_off(int b) { return b == 0 ? 0 : (b == 1 ? 2 : (b == 2 ? 10 : 13 + 2 * (b - 3))); }
+
+// Bucket B of one row: its action (argmax or Gumbel-max sample) and the
+// log-prob term logit[a] - logsumexp(bucket).
+template <int B>
+BB_HD void pol_bucket_term(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
+                           int32_t *act, float *term)
+{
+    constexpr int o = pol_bucket_off(B), nb = pol_bucket(B);
+    float mx = logit[o];
+#pragma unroll
+    for (int i = 1; i < nb; i++) mx = logit[o + i] > mx ? logit[o + i] : mx;
+    int a = 0;
+    if (stochastic) {
+        float best = logit[o] + pol_gumbel(seed, step, row, (uint32_t)o);
+#pragma unroll
+        for (int i = 1; i < nb; i++) {
+            const float g = logit[o + i] + pol_gumbel(seed, step, row, (uint32_t)(o + i));
+            if (g > best) { best = g; a = i; }
+        }
+    } else {
+        float best = logit[o];
+#pragma unroll
+        for (int i = 1; i < nb; i++)
+            if (logit[o + i] > best) { best = logit[o + i]; a = i; }  // first maximum (torch argmax)
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < nb; i++) s = s + pol_expf(logit[o + i] - mx);
+    const float lse = mx + pol_logf(s);
+    float la = logit[o];
+#pragma unroll
+    for (int i = 1; i < nb; i++) la = a == i ? logit[o + i] : la;
+    *act = a;
+    *term = la - lse;
+}
+
+// Summed log-prob of the six bucket terms, in bucket order.
+BB_HD float pol_logp_sum(const float (&term)[POL_BUCKETS])
+{
+    float total = 0.f;
+#pragma unroll
+    for (int b = 0; b < POL_BUCKETS; b++) total = total + term[b];
+    return total;
+}
+
+// Bucket sampling / scoring of one row's logits (fully unrolled: the bucket
+// sizes and offsets are compile-time, so logit[] stays in registers).
 BB_HD void pol_select(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
                       int32_t act[6], float *logp_sum)
 {
-    int o = 0;
-    float total = 0.f;
-#pragma unroll
-    for (int b = 0; b < POL_BUCKETS; b++) {
-        const int nb = pol_bucket(b);
-        float mx = logit[o];
-#pragma unroll
-        for (int i = 1; i < nb; i++) mx = logit[o + i] > mx ? logit[o + i] : mx;
-        int a = 0;
-        if (stochastic) {
-            float best = logit[o] + pol_gumbel(seed, step, row, (uint32_t)o);
-#pragma unroll
-            for (int i = 1; i < nb; i++) {
-                const float g = logit[o + i] + pol_gumbel(seed, step, row, (uint32_t)(o + i));
-                if (g > best) { best = g; a = i; }
-            }
-        } else {
-            float best = logit[o];
-#pragma unroll
-            for (int i = 1; i < nb; i++)
-                if (logit[o + i] > best) { best = logit[o + i]; a = i; }  // first maximum (torch argmax)
-        }
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < nb; i++) s = s + pol_expf(logit[o + i] - mx);
-        const float lse = mx + pol_logf(s);
-        float la = logit[o];
-#pragma unroll
-        for (int i = 1; i < nb; i++) la = a == i ? logit[o + i] : la;
-        total = total + (la - lse);
-        act[b] = a;
-        o += nb;
-    }
-    *logp_sum = total;
+    float term[POL_BUCKETS];
+    pol_bucket_term<0>(logit, stochastic, seed, step, row, &act[0], &term[0]);
+    pol_bucket_term<1>(logit, stochastic, seed, step, row, &act[1], &term[1]);
+    pol_bucket_term<2>(logit, stochastic, seed, step, row, &act[2], &term[2]);
+    pol_bucket_term<3>(logit, stochastic, seed, step, row, &act[3], &term[3]);
+    pol_bucket_term<4>(logit, stochastic, seed, step, row, &act[4], &term[4]);
+    pol_bucket_term<5>(logit, stochastic, seed, step, row, &act[5], &term[5]);
+    *logp_sum = pol_logp_sum(term);
 }
 
 // Sum of 32 values in the kernel's order: t_c = v_c + v_{c+16}, then the xor

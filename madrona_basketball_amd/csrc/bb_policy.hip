@@ -15,6 +15,7 @@
 // The C/D layout (col = l & 15, row = 4q + i) puts a row's 32 outputs on the 16
 // lanes of one quarter-wave: LayerNorm is a 4-step xor butterfly there.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include "bb_launch.h"
 #include "bb_policy.h"
 
@@ -24,9 +25,6 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // 16-row MFMA blocks per tile: 4 -> 64 rows per wave pass, one row per lane in the bucket pass
 // (measured 25.2 us for 65 536 argmax rows vs 29.9 at 2 blocks and 2 waves per SIMD)
-#ifndef POLICY_MT
-#define POLICY_MT 4
-#endif
 
 // Sum over the 16 lanes of a DPP row, the same tree as bb_policy.h pol_sum32's
 // xor butterfly (partners 1, 2, then the other quad / half: once a quad holds
@@ -62,9 +60,136 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
     }
 }
 
+// Ordering of LDS words written and read by different lanes of the wave.
+__device__ __forceinline__ void pol_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Bucket pass of a tile of R = 16 MT < 64 rows: LPR = 64 / R lanes per row,
+// every step the same instructions on different data (no divergent roles):
+//   A  lane part p: the Gumbel noise of logit pairs p, p + LPR, ... (one
+//      threefry call per pair) and, per logit, g = logit + noise and
+//      e = exp(logit - bucket max), into LDS;
+//   B  lane part p: buckets p, p + LPR, ...: first maximum of g, sum of e in
+//      logit order, logit - logsumexp, into LDS;
+//   C  lane part 0: the six terms summed in bucket order, the outputs.
+// Every value is the one pol_bucket_term / pol_select computes (same
+// operations on the same inputs), so rows are bit-identical to MT = 4's.
+template <int MT>
+__device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane)
+{
+    constexpr int R = 16 * MT, LPR = 64 / R;
+    constexpr int PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    __shared__ float gbuf[R][POL_LOGITS + 1], ebuf[R][POL_LOGITS + 1], tbuf[R][POL_BUCKETS];
+    __shared__ int32_t abuf[R][POL_BUCKETS];
+    const int r = lane / LPR, part = lane % LPR;
+    const int64_t rr = row0 + r;
+    const bool live = rr < a.rows;
+    const bool stochastic = a.stochastic != 0;
+    const float *lg = tile[r];
+    // bucket maxima (every lane, compile-time indices)
+    float mx[POL_BUCKETS];
+#pragma unroll
+    for (int b = 0; b < POL_BUCKETS; b++) {
+        const int o = pol_bucket_off(b), nb = pol_bucket(b);
+        float m = lg[o];
+        for (int i = 1; i < nb; i++) m = lg[o + i] > m ? lg[o + i] : m;
+        mx[b] = m;
+    }
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+        const int pr = part + LPR * j;
+        if (pr < PAIRS) {
+            uint32_t b0 = 0, b1 = 0;
+            if (stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int i = 2 * pr + h;
+                if (i < POL_LOGITS) {
+                    const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
+                    float m = mx[0];
+#pragma unroll
+                    for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
+                    const float x = lg[i];
+                    // pol_gumbel's value for logit i (its threefry word h)
+                    const float g = stochastic ? x + (-pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)))) : x;
+                    gbuf[r][i] = g;
+                    ebuf[r][i] = pol_expf(x - m);
+                }
+            }
+        }
+    }
+    pol_wave_sync();
+#pragma unroll
+    for (int j = 0; j < BPL; j++) {
+        const int b = part + LPR * j;
+        if (b < POL_BUCKETS) {
+            const int o = pol_bucket_off(b), nb = pol_bucket(b);
+            float best = gbuf[r][o], s = ebuf[r][o];
+            int act = 0;
+#pragma unroll
+            for (int i = 1; i < 8; i++) {
+                if (i < nb) {
+                    const float g = gbuf[r][o + i];
+                    if (g > best) { best = g; act = i; }  // first maximum
+                    s = s + ebuf[r][o + i];
+                }
+            }
+            float m = mx[0];
+#pragma unroll
+            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
+            const float lse = m + pol_logf(s);
+            abuf[r][b] = act;
+            tbuf[r][b] = lg[o + act] - lse;
+        }
+    }
+    pol_wave_sync();
+    if (part == 0 && live) {
+        float term[POL_BUCKETS];
+        int32_t act[POL_BUCKETS];
+#pragma unroll
+        for (int b = 0; b < POL_BUCKETS; b++) { term[b] = tbuf[r][b]; act[b] = abuf[r][b]; }
+        const float lp = pol_logp_sum(term);
+        if (a.actions) {
+            int32_t *d = a.actions + rr * a.act_stride;
+#pragma unroll
+            for (int b = 0; b < 6; b++) d[b] = act[b];
+        }
+        if (a.act_out) {
+            int2 *d = (int2 *)(a.act_out + rr * 6);
+            d[0] = make_int2(act[0], act[1]);
+            d[1] = make_int2(act[2], act[3]);
+            d[2] = make_int2(act[4], act[5]);
+        }
+        if (a.log_prob) a.log_prob[rr] = lp;
+        if (a.value) a.value[rr] = lg[POL_LOGITS];
+        if (a.rew_out) {  // the previous step's outcome of this row (buffer.rewards / not_dones)
+            a.rew_out[rr] = a.rew_src[rr * a.rd_stride];
+            a.done_out[rr] = a.done_src[rr * a.rd_stride];
+        }
+    }
+}
+
+// diagnostics (PolicyArgs::diag_ts): the clock at phase boundaries of the
+// wave's first tile -- 0 start, 1 weights loaded, 2 rows loaded, 3 layer 1,
+// 4 layer 2 + heads, 5 bucket pass done
+__device__ __forceinline__ void pol_trace(const PolicyArgs &a, bool first, int point, bool wait_mem)
+{
+    if (a.diag_ts && first) {
+        if (wait_mem) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = wall_clock64();
+        if (threadIdx.x == 0) a.diag_ts[(int64_t)blockIdx.x * POL_TRACE_POINTS + point] = t;
+    }
+}
+
+template <int MT>
 __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
 {
-    constexpr int MT = POLICY_MT;  // 16-row M-tiles per tile
+    pol_trace(a, true, 0, false);
+    // MT: 16-row M-tiles per tile
     __shared__ __attribute__((aligned(16))) float norm[2][POL_IN];
     __shared__ float tile[16 * MT][33];
     const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
@@ -95,10 +220,12 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
     const float l2b0 = W.ln2_b[c], l2b1 = W.ln2_b[c + 16];
     const float bh0 = W.head_b[c], bh1 = W.head_b[c + 16];
     __syncthreads();
+    pol_trace(a, true, 1, true);
 
     const int64_t tiles = (a.rows + 16 * MT - 1) / (16 * MT);
     for (int64_t tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
         const int64_t row0 = tl * 16 * MT;
+        const bool first = tl == blockIdx.x;
         // every M-tile's 32 observation floats per lane, loads issued together
         float x[MT][32];
 #pragma unroll
@@ -122,6 +249,7 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
                 for (int j = 0; j < 32; j++) x[m][j] = 0.f;
             }
         }
+        pol_trace(a, first, 2, true);
         // layer 1 (two independent accumulators per M-tile keep the MFMA pipe full)
         float nm[32], ni[32];
 #pragma unroll
@@ -148,6 +276,7 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
             ln_relu_to_tile(a0, a1, b1_0, b1_1, l1w0, l1w1, l1b0, l1b1, tile + 16 * m, c, q);
         }
         __syncthreads();
+        pol_trace(a, first, 3, false);
         // layer 2 and heads, per M-tile through its 16 rows of the tile
 #pragma unroll
         for (int m = 0; m < MT; m++) {
@@ -181,6 +310,13 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
             }
         }
         __syncthreads();
+        pol_trace(a, first, 4, false);
+        if constexpr (16 * MT < 64) {
+            bucket_pass_spread<MT>(a, tile, row0, lane);
+            __syncthreads();
+            pol_trace(a, first, 5, false);
+            continue;
+        }
         // one row per lane: buckets, log-prob, value
         const int64_t rr = row0 + lane;
         if (lane < 16 * MT && rr < a.rows) {
@@ -212,13 +348,43 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
     }
 }
 
+// M-tiles per wave.  4: 64 rows per wave, one row per lane in the bucket
+// pass, each lane's 19 Gumbel draws in series; 1: 16 rows per wave, 4 lanes
+// per row in the bucket pass.  Measured (profiles/r03/e_policy_mt_ab.txt):
+// 8 192 rows 18.1 (MT 4) -> 13.9-18.6 us (MT 1), 65 536 rows 24.8 (MT 4) vs
+// 28.8 us (MT 1): MT = 1 below POLICY_MT4_ROWS rows.  MADRONA_BB_POLICY_MT
+// forces one (A/B timing).
+#ifndef POLICY_MT4_ROWS
+#define POLICY_MT4_ROWS 32768
+#endif
+inline int policy_mt(int64_t rows)
+{
+    static const int forced = [] {
+        const char *e = getenv("MADRONA_BB_POLICY_MT");
+        const int m = e && *e ? atoi(e) : 0;
+        return (m == 1 || m == 2 || m == 4) ? m : 0;
+    }();
+    if (forced) return forced;
+    return rows < POLICY_MT4_ROWS ? 1 : 4;
+}
+
+template <int MT>
+static hipError_t launch_policy_mt(const PolicyArgs &a, hipStream_t s)
+{
+    const int64_t tiles = (a.rows + 16 * MT - 1) / (16 * MT);
+    if (tiles <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)(tiles < 16384 ? tiles : 16384);  // grid-stride beyond
+    hipLaunchKernelGGL(k_policy<MT>, dim3(grid), dim3(64), 0, s, a);
+    return hipGetLastError();
+}
+
 hipError_t launch_policy(const PolicyArgs &a, hipStream_t s)
 {
-    const int64_t tiles = (a.rows + 16 * POLICY_MT - 1) / (16 * POLICY_MT);
-    if (tiles <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)(tiles < 4096 ? tiles : 4096);  // grid-stride beyond
-    hipLaunchKernelGGL(k_policy, dim3(grid), dim3(64), 0, s, a);
-    return hipGetLastError();
+    switch (policy_mt(a.rows)) {
+    case 1: return launch_policy_mt<1>(a, s);
+    case 2: return launch_policy_mt<2>(a, s);
+    default: return launch_policy_mt<4>(a, s);
+    }
 }
 
 void host_policy(const PolicyArgs &a)

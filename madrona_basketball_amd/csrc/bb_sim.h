@@ -2084,11 +2084,15 @@ BB_HD void store_world_shared(const World<N> &s, const Params &p, int64_t w, con
 // Per-agent columns of agent i (row w*N + i of every [W][N][...] column).
 // Team changes only inside generate/reset, which write it directly.  With
 // `o` (agent i's event-only words as loaded) those are rewritten only when
-// changed.
-template <int N, int CA = -1>
+// changed.  PART: STORE_ALL, or one of the two halves a kernel may store
+// from different waves (STORE_ACT_ATTR: Action + Attributes, the columns the
+// defence AI and the shot percentage write; STORE_REST: all the others).
+enum StorePart : int { STORE_ALL = 0, STORE_ACT_ATTR = 1, STORE_REST = 2 };
+template <int N, int CA = -1, int PART = STORE_ALL>
 BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int i, const OrigAgent *o = nullptr)
 {
     const Columns &c = p.c;
+    constexpr bool AA = PART != STORE_REST, REST = PART != STORE_ACT_ATTR;
     uint32_t a[6], m[4], pos[3], ps[3], q[4], v[3], ib[2], at[10];
 #pragma unroll
     for (int k = 0; k < 6; k++) a[k] = (uint32_t)s.act[i][k];
@@ -2101,18 +2105,23 @@ BB_HD void store_world_agent(const World<N> &s, const Params &p, int64_t r, int 
     ib[0] = (uint32_t)s.inb[i]; ib[1] = (uint32_t)s.allow[i];
 #pragma unroll
     for (int k = 0; k < 10; k++) at[k] = fbits(s.attr[i][k]);
-    if (!o || s.rst[i] != o->rst) c.reset[r] = s.rst[i];
-    store_words<6, CA>(c.action, r, a);
-    store_words<4, CA>(c.action_mask, r, m);
-    store_words<3, CA>(c.agent_pos, r, pos);
-    c.reward[r] = s.rew[i];
-    c.done[r] = s.done[i];
-    store_words<3, CA>(c.possession, r, ps);
-    store_words<4, CA>(c.orientation, r, q);
-    store_words<3, CA>(c.agent_vel, r, v);
-    c.cooldown[r] = s.cd[i];
-    c.cur_step[r] = s.step[i];
-    if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2, CA>(c.inbounding, r, ib);
+    if (REST) {
+        if (!o || s.rst[i] != o->rst) c.reset[r] = s.rst[i];
+    }
+    if (AA) store_words<6, CA>(c.action, r, a);
+    if (REST) {
+        store_words<4, CA>(c.action_mask, r, m);
+        store_words<3, CA>(c.agent_pos, r, pos);
+        c.reward[r] = s.rew[i];
+        c.done[r] = s.done[i];
+        store_words<3, CA>(c.possession, r, ps);
+        store_words<4, CA>(c.orientation, r, q);
+        store_words<3, CA>(c.agent_vel, r, v);
+        c.cooldown[r] = s.cd[i];
+        c.cur_step[r] = s.step[i];
+        if (!o || s.inb[i] != o->inb || s.allow[i] != o->allow) store_words<2, CA>(c.inbounding, r, ib);
+    }
+    if (!AA) return;
     bool attr_ev = o == nullptr || BB_FULL_ROWS;
     if (o) {
 #pragma unroll

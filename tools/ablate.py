@@ -85,10 +85,25 @@ def trace(L, sim, stream):
     nw = ctypes.c_int64()
     rc = L.bb_diag_trace(sim._h, stream, buf.ctypes.data, cap, ctypes.byref(nw))
     assert rc == 0, L.bb_last_error()
+    pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
+    ngrid = (sim.num_worlds * sim.num_agents + 63) // 64
+    if nw.value != ngrid:  # k_step_wide: WAVES waves per workgroup, per-role phases
+        waves = nw.value // ngrid
+        t = buf[: nw.value, :10].astype(np.int64).reshape(ngrid, waves, 10)
+        t -= t[:, :, 0].min()
+        roles = ["DEF", "PCT", "STORE"] + [f"OBS{i}" for i in range(waves - 3)]
+        res = {"waves": int(nw.value), "tick_ns": 10, "kernel_span": int(t[:, :, 9].max() - t[:, :, 0].min())}
+        for r, name in enumerate(roles):
+            x = t[:, r]
+            res[name] = {"start": pct(x[:, 0]), "load": pct(x[:, 1] - x[:, 0]), "b0_wait": pct(x[:, 2] - x[:, 1]),
+                         "systems": pct(x[:, 3] - x[:, 2]), "b1_wait": pct(x[:, 4] - x[:, 3]),
+                         "tail": pct(x[:, 9] - x[:, 4]), "end": pct(x[:, 9])}
+        for k, v in res.items():
+            print(f"trace {k:6s} {v}", flush=True)
+        return res
     t = buf[: nw.value, :10].astype(np.int64)
     resets = buf[: nw.value, 10].astype(np.int64)
     t -= t[:, 0].min()
-    pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
     names = ["load", "tick..move", "grab..shoot", "ball..score", "oob..inbound", "reset", "points..defense",
              "reward+store", "obs"]
     res = {"waves": int(nw.value), "tick_ns": 10, "start_pct": pct(t[:, 0]), "end_pct": pct(t[:, 9]),

@@ -45,6 +45,9 @@ def main():
     for b, n in NAMES.items():
         x = t(5, 1 << b)
         print(f"  without {n:12s} {x:8.2f} us   saves {base - x:6.2f} us")
+    for combo in ((8, 17), (8, 17, 6), (6, 8)):
+        x = t(5, sum(1 << b for b in combo))
+        print(f"  without {'+'.join(NAMES[b] for b in combo):24s} {x:8.2f} us   saves {base - x:6.2f} us")
     allsys = t(5, sum(1 << b for b in NAMES))
     print(f"  without all systems {allsys:.2f} us")
     for b, n in NAMES.items():

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--worlds", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--only-argmax", action="store_true", help="agent-0 rows, argmax only (PMC runs)")
+    ap.add_argument("--trace", action="store_true", help="per-wave phase clocks of one launch (agent-0 rows)")
     a = ap.parse_args()
     import madrona_basketball_amd as mba
     from madrona_basketball_amd.policy import FusedPolicy, make_agent
@@ -28,6 +29,32 @@ def main():
     cases = [("agent 0 rows", obs_all[:, 0])]
     if not a.only_argmax:
         cases.append(("all agents", obs_all.view(-1, obs_all.shape[-1])))
+    if a.trace:
+        import ctypes
+        import numpy as np
+        from madrona_basketball_amd import _lib
+        L = _lib.load()
+        L.bb_diag_policy_trace.restype = ctypes.c_int
+        L.bb_diag_policy_trace.argtypes = [ctypes.POINTER(_lib.PolicyWeights), ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+        obs = obs_all[:, 0]
+        for stoch in (0, 1):
+            buf = np.zeros((1 << 16, 8), np.uint64)
+            nw = ctypes.c_int64()
+            rc = L.bb_diag_policy_trace(ctypes.byref(pol._w), 0, obs.data_ptr(), obs.shape[0], obs.stride(0), stoch,
+                                        torch.cuda.current_stream().cuda_stream, buf.ctypes.data, buf.shape[0],
+                                        ctypes.byref(nw))
+            assert rc == 0, L.bb_last_error()
+            t = buf[:, :6].astype(np.int64)
+            t = t[t[:, 0] > 0]
+            t -= t[:, 0].min()
+            pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
+            names = ["weights", "rows", "layer1", "layer2+heads", "buckets"]
+            print(f"trace rows {obs.shape[0]} stochastic={stoch} waves {len(t)} (10 ns ticks) start {pct(t[:, 0])} "
+                  f"end {pct(t[:, 5])}", flush=True)
+            for i, n in enumerate(names):
+                print(f"  {n:14s} {pct(t[:, i + 1] - t[:, i])}", flush=True)
     for label, obs in cases:
         rows = obs.shape[0]
         act = torch.empty((rows, 6), dtype=torch.int32, device="cuda")
