@@ -240,6 +240,9 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
  * Sampling as bb_policy_forward with step = step0 + k (stochastic = 0: argmax);
  * the opponent samples with seed ^ 0x9E3779B9.  Equal, bit for bit, to n x
  * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
+ * On gfx950 without an opponent (and up to 8 192 worlds) one fused launch
+ * runs all n steps; flags BB_ROLLOUT_PER_STEP forces a policy launch and a
+ * step launch per step instead.
  * kernel_ms (CUDA mode): time from the first launch to the last, after a sync. */
 typedef struct bb_policy_rollout_buffers {
     float *obs;
@@ -248,7 +251,7 @@ typedef struct bb_policy_rollout_buffers {
 } bb_policy_rollout_buffers;
 int bb_rollout_policy(bb_sim *sim, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
                       int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
-                      const bb_policy_rollout_buffers *out, void *stream, float *kernel_ms);
+                      const bb_policy_rollout_buffers *out, uint32_t flags, void *stream, float *kernel_ms);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

@@ -111,7 +111,7 @@ def load():
                                              i32, u32, u32, vp]),
         "bb_record": (ctypes.c_int, [vp, i64, i32, vp, i64, vp]),
         "bb_rollout_policy": (ctypes.c_int, [vp, ctypes.POINTER(PolicyWeights), ctypes.POINTER(PolicyWeights), i32,
-                                             i32, i32, u32, u32, ctypes.POINTER(PolicyRolloutBuffers), vp,
+                                             i32, i32, u32, u32, ctypes.POINTER(PolicyRolloutBuffers), u32, vp,
                                              ctypes.POINTER(ctypes.c_float)]),
         "bb_set_action": (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, i32, vp]),
         "bb_trigger_reset": (ctypes.c_int, [vp, i32, vp]),

@@ -217,6 +217,13 @@ hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStrea
 #undef CALL
 }
 
+hipError_t launch_rollout_policy(int n, const Params &p, const PolicyRolloutArgs &r, hipStream_t s)
+{
+#define CALL(k) launch_rollout_policy_t<k>(p, r, s)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
 bool fused_rollout_n(int n)
 {
     switch (n) {

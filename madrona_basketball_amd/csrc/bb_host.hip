@@ -812,10 +812,25 @@ bb::PolicyWeights policy_weights(const bb_policy_weights *w)
 
 }  // namespace
 
+// The fused PPO rollout (k_rollout_policy) runs one workgroup of 3 waves per
+// 32 worlds at one workgroup per CU (register-bound): used up to two waves of
+// workgroups -- measured 8 192 worlds 15.1 vs 27.6 us per step unfused,
+// 16 384: 29.7 vs 33.4, 65 536: 115 vs 64 (profiles/r03/g_ppo_fused_ab.txt).
+// MADRONA_BB_PPO_FUSED_MAX_WORLDS overrides the bound.
+static int64_t ppo_fused_max_worlds()
+{
+    static const int64_t v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_FUSED_MAX_WORLDS");
+        return (int64_t)(e && *e ? std::atoll(e) : 16384);
+    }();
+    return v;
+}
+
 int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
                       int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
-                      const bb_policy_rollout_buffers *out, void *stream, float *kernel_ms)
+                      const bb_policy_rollout_buffers *out, uint32_t flags, void *stream, float *kernel_ms)
 {
+    if (flags & ~BB_ROLLOUT_PER_STEP) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: unknown flag bits");
     if (!s || n < 0 || !out) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: arguments");
     if (kernel_ms) *kernel_ms = 0.f;
     if (!weights_ok(w) || (opponent && !weights_ok(opponent)))
@@ -885,13 +900,42 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             return fail(BB_ERR_HIP, "hipEventCreate");
         (void)hipEventRecord(e0, st);
     }
-    for (int32_t k = 0; k < n; k++) {
+    const bool fused = !(flags & BB_ROLLOUT_PER_STEP) && !opponent && bb::fused_rollout_n(s->n) &&
+                       W <= ppo_fused_max_worlds();
+    if (fused) {
+        bb::PolicyRolloutArgs r{};
+        r.w = policy_weights(w);
+        r.obs_out = out->obs; r.act_out = out->actions; r.log_prob = out->log_prob; r.value = out->value;
+        r.reward = out->reward; r.done = out->done; r.next_value = out->next_value;
+        r.steps = n; r.trainee = trainee; r.stochastic = stochastic ? 1 : 0; r.seed = seed; r.step0 = step0;
+        uint64_t *ts = nullptr;
+        const char *tr = std::getenv("MADRONA_BB_PPO_TRACE");  // diagnostics: per-step clocks of workgroup 0
+        if (tr && *tr && hipMalloc(&ts, (size_t)n * 4 * 8) == hipSuccess) r.diag_ts = ts;
+        hipError_t e = bb::launch_rollout_policy(s->n, s->p, r, st);
+        if (e != hipSuccess) return hip_fail(e, "launch fused PPO rollout kernel");
+        if (ts) {
+            std::vector<uint64_t> h((size_t)n * 4);
+            if (hipMemcpyAsync(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess) {
+                FILE *f = std::fopen(tr, "a");
+                if (f) {
+                    for (int32_t k = 0; k < n; k++)
+                        std::fprintf(f, "%d %llu %llu %llu %llu\n", k, (unsigned long long)h[4 * k],
+                                     (unsigned long long)h[4 * k + 1], (unsigned long long)h[4 * k + 2],
+                                     (unsigned long long)h[4 * k + 3]);
+                    std::fclose(f);
+                }
+            }
+            (void)hipFree(ts);
+        }
+    }
+    for (int32_t k = 0; k < (fused ? 0 : n); k++) {
         hipError_t e = bb::launch_policy(pass(k, false), st);
         if (e == hipSuccess && opponent) e = bb::launch_policy(opp_pass(k), st);
         if (e == hipSuccess) e = bb::launch_step(s->n, s->p, st);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
     }
-    if (final_needed) {
+    if (final_needed && !fused) {
         hipError_t e = bb::launch_policy(pass(n, true), st);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
     }

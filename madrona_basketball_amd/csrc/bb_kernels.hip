@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <type_traits>
 #include "bb_launch.h"
+#include "bb_policy_dev.h"
 #include "bb_sim.h"
 
 #ifndef BB_N
@@ -939,6 +940,236 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
     }
 }
 
+// ------------------------------------------------------------------ PPO rollout
+// scripts/ppo.py:61-141 in one launch (bb_rollout_policy, N = 2): a workgroup
+// of 1 + PPO_PWAVES waves per 32 worlds.  Wave S holds the worlds in
+// registers for all K steps (rollout_agent_lanes' discipline); the policy
+// waves P hold the network's B operands in registers (k_policy's) and own 16
+// trainee rows each.  Per step k:
+//   P: record the trainee's observation X (LDS) into obs_out[k], the network
+//      on X (policy_layers / bucket_pass_spread, bit-identical to k_policy),
+//      actions into LDS and act_out[k], log-prob and value;   -> barrier
+//   S: the trainee's action from LDS (the other agent keeps what the sim left
+//      in its action column), systems 1-17 and reward, reward / done of the
+//      trainee into reward[k] / done[k], the trainee's next observation row
+//      into X (and on the last step every row into the sim's tensor);  -> barrier
+// then P's value pass over the final X gives next_value (ppo.py:136-137), and S
+// stores every column of the worlds (the state after step K-1).
+constexpr int PPO_PWAVES = 2;
+constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
+struct PpoLds {
+    float x[32][PPO_XS];
+    int32_t act[32][6];
+    float norm[2][POL_IN];
+    float ptile[PPO_PWAVES][16][33];
+    BucketLds<1> bucket[PPO_PWAVES];
+    double erf[ERF_WORDS];
+};
+
+// RowSink into an LDS row (X)
+struct LdsRowSink {
+    float *row;
+    float b0, b1, b2, b3;
+    int idx;
+    __device__ void put(float v)
+    {
+        switch (idx & 3) {
+        case 0: b0 = v; break;
+        case 1: b1 = v; break;
+        case 2: b2 = v; break;
+        default: *(float4 *)(row + (idx & ~3)) = make_float4(b0, b1, b2, v); break;
+        }
+        idx++;
+    }
+    __device__ void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    __device__ void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+    __device__ void finish() { while (idx & 3) put(0.f); }
+};
+
+// diagnostics (PolicyRolloutArgs::diag_ts, workgroup 0): per step k the clock
+// at 0 S starts the step, 1 S's systems + reward done, 2 S's observation rows
+// done, 3 the first policy wave's actions done (for step k)
+__device__ __forceinline__ void ppo_trace(const PolicyRolloutArgs &r, int t, int point)
+{
+    if (r.diag_ts && blockIdx.x == 0) {
+        const uint64_t c = wall_clock64();
+        if (threadIdx.x % WAVE == 0) r.diag_ts[(int64_t)t * 4 + point] = c;
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, float *tile)
+{
+    using T = StepTile<N, false>;
+    const int lane = threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const int wl = lane / N;
+    const bool active = w < p.num_worlds;
+    const int trainee = r.trainee;
+    World<N> v;
+    if (active) {
+        World<N> s;
+        load_world(s, p, w);
+        agent_view(s, v, lane % N);
+    }
+    {
+        const double *g = &bbm::ERF_TAYLOR[0][0];
+#pragma unroll
+        for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
+            const int i = j * WAVE + lane;
+            if (i < ERF_WORDS) L.erf[i] = g[i];
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load pending into the loop
+    __syncthreads();  // setup: X holds the trainee rows of step 0, the erf table is in LDS
+    for (int t = 0; t < r.steps; t++) {
+        int lane_t = lane;
+        int64_t w_t = w;
+        __asm__ volatile("" : "+v"(lane_t));
+        __asm__ volatile("" : "+v"(w_t));
+        const int k = lane_t % N;
+        Ctx c = make_ctx(p, w_t, k == 0);
+        c.erf_tab = L.erf;
+        const LaneAgents<N, MODE_FULL> ag{k, &p};
+        __syncthreads();  // the policy's actions are in LDS
+        ppo_trace(r, t, 0);
+        int32_t ib = -1;
+        bool share = false;
+        if (active) {
+            World<N> s;
+            agent_view<N, true>(v, s, k);
+            int32_t a[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) a[q] = L.act[wl][q];
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) s.act[i][q] = i == trainee ? a[q] : s.act[i][q];
+            step_world_pre_obs(s, c, ag);
+            ib = inbounder_id(s);
+            share = obs_sharable(s);
+            agent_view(s, v, k);
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            ppo_trace(r, t, 1);
+            if (k == trainee) {
+                if (r.reward) {
+                    r.reward[(int64_t)t * p.num_worlds + w_t] = v.rew[0];
+                    r.done[(int64_t)t * p.num_worlds + w_t] = v.done[0];
+                }
+            }
+        }
+        // the trainee's next observation row into X
+        {
+            SharedObs<N> sh;
+            lane_shared_obs(v, c, active, sh);
+            if (active && k == trainee) {
+                float *xr = L.x[wl];
+                if (share) {
+                    LdsRowSink o;
+                    o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                    emit_row_shared(v, c, sh, 0, o, ib);
+                } else if (canonical_slots(v, 0)) {
+                    LdsRowSink o;
+                    o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+                    emit_row_fast(v, c, 0, o, ib);
+                } else {
+                    fill_obs_slow(v, c, 0, xr, ib);
+                }
+            }
+        }
+        if (t + 1 == r.steps) {  // the sim's observation tensor: every row of the last step
+            wide_obs_pass<N, 0>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
+            wave_sync();
+            wide_obs_pass<N, 1>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
+        }
+        wave_sync();
+        ppo_trace(r, t, 2);
+        __syncthreads();  // X holds the observations after step t
+    }
+    if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
+        int64_t w_s = w;
+        __asm__ volatile("" : "+v"(w_s));
+        const int k = lane % N;
+        store_world_agent(v, p, w_s * N + k, 0);
+        if (k == 0) store_world_shared(v, p, w_s);
+    }
+}
+
+__device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
+{
+    const int lane = threadIdx.x % WAVE, c = lane & 15, q = lane >> 4;
+    const int64_t W = p.num_worlds;
+    const int r0 = 16 * pw;                                   // first X row of this wave
+    const int64_t row0 = (int64_t)blockIdx.x * 32 + r0;       // its first world
+    float (*tile)[33] = L.ptile[pw];
+    // network constants: norm by the lanes of both policy waves, B operands per lane
+    for (int k = pw * WAVE + lane; k < POL_IN; k += PPO_PWAVES * WAVE) {
+        L.norm[0][k] = r.w.obs_mean[k];
+        L.norm[1][k] = r.w.obs_inv[k];
+    }
+    PolicyRegs R;
+    load_policy_regs(R, r.w, c, q);
+    // X for step 0: the trainee rows of the sim's observation tensor (and a
+    // zero tail, which emit never writes)
+    for (int i = lane; i < 16 * 32; i += WAVE) {
+        const int rr = i / 32, qq = i % 32;
+        const int64_t wg = row0 + rr;
+        float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (wg < W) v4 = *(const float4 *)(p.c.obs + (wg * 2 + r.trainee) * (int64_t)obs_width(2) + 4 * qq);
+        *(float4 *)&L.x[r0 + rr][4 * qq] = v4;
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();  // setup
+    PolicyArgs a{};
+    a.rows = W;
+    a.stochastic = r.stochastic;
+    a.seed = r.seed;
+    for (int t = 0; t <= r.steps; t++) {
+        const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
+        if (!final_pass && r.obs_out) {  // buffer.obs[t] = X
+            for (int i = lane; i < 16 * 32; i += WAVE) {
+                const int rr = i / 32, qq = i % 32;
+                const int64_t wg = row0 + rr;
+                if (wg < W) *(float4 *)(r.obs_out + ((int64_t)t * W + wg) * POL_IN + 4 * qq) = *(const float4 *)&L.x[r0 + rr][4 * qq];
+            }
+        }
+        float x[1][32];
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float4 o = *(const float4 *)&L.x[r0 + c][32 * q + 4 * v];
+            x[0][4 * v] = o.x; x[0][4 * v + 1] = o.y; x[0][4 * v + 2] = o.z; x[0][4 * v + 3] = o.w;
+        }
+        policy_layers<1>(x, R, L.norm, tile, c, q);
+        a.step = r.step0 + (uint32_t)t;
+        if (!final_pass) {
+            a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
+            a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
+            a.value = r.value ? r.value + (int64_t)t * W : nullptr;
+            bucket_pass_spread<1>(a, tile, row0, lane, L.bucket[pw], L.act + r0);
+            pol_wave_sync();
+            if (pw == 0) ppo_trace(r, t, 3);
+            __syncthreads();  // actions in LDS
+            __syncthreads();  // X holds the observations after step t
+        } else if (r.next_value) {
+            const int rr = lane >> 2;
+            if ((lane & 3) == 0 && row0 + rr < W) r.next_value[row0 + rr] = tile[rr][POL_LOGITS];
+        }
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), 1) void k_rollout_policy(const Params p, const PolicyRolloutArgs r)
+{
+    if constexpr (N == 2 && FusedRollout<N>::value) {
+        __shared__ PpoLds L;
+        __shared__ float4 tile4[StepTile<N, false>::FLOATS / 4];
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        if (wave == 0) ppo_sim_wave<N>(p, r, L, (float *)tile4);
+        else ppo_policy_wave(p, r, L, wave - 1);
+    }
+}
+
 // ------------------------------------------------------------------ N >= 4
 // One lane per agent; the world's state lives in LDS and its N lanes run the
 // world-level systems on it together (same instructions, same values); the
@@ -1588,6 +1819,18 @@ hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s
 }
 
 template <int N>
+hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, hipStream_t s)
+{
+    if constexpr (N != 2 || !FusedRollout<N>::value) {
+        return hipErrorNotSupported;
+    } else {
+        const dim3 grid((unsigned)((p.num_worlds + 31) / 32)), block(WAVE * (1 + PPO_PWAVES));
+        hipLaunchKernelGGL(k_rollout_policy<N>, grid, block, 0, s, p, r);
+        return hipGetLastError();
+    }
+}
+
+template <int N>
 hipError_t launch_init_t(const Params &p, hipStream_t s)
 {
     hipLaunchKernelGGL(HIP_KERNEL_NAME(k_init<N>), dim3((unsigned)((p.num_worlds + 255) / 256)), dim3(256), 0, s, p);
@@ -1597,6 +1840,7 @@ hipError_t launch_init_t(const Params &p, hipStream_t s)
 template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value; }
 template <> int step_grid<BB_N>(int64_t num_worlds)
 {

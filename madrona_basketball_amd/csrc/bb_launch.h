@@ -31,6 +31,20 @@ struct RolloutArgs {
     int32_t steps;     // K
 };
 
+// PPO rollout with the policy in the loop (bb_rollout_policy, fused kernel
+// k_rollout_policy<2>): per step the policy on the trainee rows, the step, the
+// buffer stores of scripts/ppo.py:129-134; then next_value.
+struct PolicyRolloutArgs {
+    PolicyWeights w;
+    float *obs_out;       // [K][W][128]  trainee observation before each step
+    int32_t *act_out;     // [K][W][6]    the policy's actions
+    float *log_prob, *value, *reward, *done;  // [K][W]
+    float *next_value;    // [W]
+    int32_t steps, trainee, stochastic;
+    uint32_t seed, step0;
+    uint64_t *diag_ts;    // diagnostics only: per-step phase clocks of workgroup 0 ([steps][4])
+};
+
 // Trajectory recorder (bb_record): NSEG column segments per recorded world.
 constexpr int RECORD_SEGS = 10;
 struct RecordArgs {
@@ -47,13 +61,15 @@ template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= wav
 template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
                                              hipEvent_t ev1);
 template <int N> bool fused_rollout();  // k_rollout<N> exists (else: one k_step launch per step)
+template <int N> hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, hipStream_t s);
 
 #define BB_EXTERN_N(n)                                                                  \
     extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t); \
     extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);           \
     template <> int step_grid<n>(int64_t);                                              \
     extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
-    template <> bool fused_rollout<n>();
+    template <> bool fused_rollout<n>();                                                \
+    extern template hipError_t launch_rollout_policy_t<n>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 BB_EXTERN_N(2)
 BB_EXTERN_N(4)
 BB_EXTERN_N(6)
@@ -67,6 +83,8 @@ hipError_t launch_init(int n, const Params &p, hipStream_t s);
 hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
                           hipEvent_t ev1 = nullptr);
 bool fused_rollout_n(int n);
+// fused PPO rollout (N = 2 only; hipErrorNotSupported otherwise)
+hipError_t launch_rollout_policy(int n, const Params &p, const PolicyRolloutArgs &r, hipStream_t s);
 int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);

@@ -18,160 +18,9 @@
 #include <cstdlib>
 #include "bb_launch.h"
 #include "bb_policy.h"
+#include "bb_policy_dev.h"
 
 namespace bb {
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// 16-row MFMA blocks per tile: 4 -> 64 rows per wave pass, one row per lane in the bucket pass
-// (measured 25.2 us for 65 536 argmax rows vs 29.9 at 2 blocks and 2 waves per SIMD)
-
-// Sum over the 16 lanes of a DPP row, the same tree as bb_policy.h pol_sum32's
-// xor butterfly (partners 1, 2, then the other quad / half: once a quad holds
-// equal values any cross-quad partner gives the same bits): four DPP adds.
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x)
-{
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
-}
-__device__ __forceinline__ float quarter_sum(float t)
-{
-    t = t + dpp_f<0xB1>(t);   // quad_perm [1,0,3,2]: xor 1
-    t = t + dpp_f<0x4E>(t);   // quad_perm [2,3,0,1]: xor 2
-    t = t + dpp_f<0x141>(t);  // row_half_mirror: the other quad of the 8
-    t = t + dpp_f<0x140>(t);  // row_mirror: the other 8 of the 16
-    return t;
-}
-
-// LayerNorm + ReLU of the 4 rows a lane holds (cols c and c + 16), then the
-// result into the LDS tile [row][col].
-__device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0, float bias1, float w0, float w1,
-                                                float lb0, float lb1, float (*tile)[33], int c, int q)
-{
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
-        const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
-        const float d0 = h0 - mean, d1 = h1 - mean;
-        const float var = quarter_sum((d0 * d0) + (d1 * d1)) * (1.0f / 32.0f);
-        const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
-        tile[4 * q + i][c] = pol_relu(((d0 * inv) * w0) + lb0);
-        tile[4 * q + i][c + 16] = pol_relu(((d1 * inv) * w1) + lb1);
-    }
-}
-
-// Ordering of LDS words written and read by different lanes of the wave.
-__device__ __forceinline__ void pol_wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-// Bucket pass of a tile of R = 16 MT < 64 rows: LPR = 64 / R lanes per row,
-// every step the same instructions on different data (no divergent roles):
-//   A  lane part p: the Gumbel noise of logit pairs p, p + LPR, ... (one
-//      threefry call per pair) and, per logit, g = logit + noise and
-//      e = exp(logit - bucket max), into LDS;
-//   B  lane part p: buckets p, p + LPR, ...: first maximum of g, sum of e in
-//      logit order, logit - logsumexp, into LDS;
-//   C  lane part 0: the six terms summed in bucket order, the outputs.
-// Every value is the one pol_bucket_term / pol_select computes (same
-// operations on the same inputs), so rows are bit-identical to MT = 4's.
-template <int MT>
-__device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane)
-{
-    constexpr int R = 16 * MT, LPR = 64 / R;
-    constexpr int PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
-    __shared__ float gbuf[R][POL_LOGITS + 1], ebuf[R][POL_LOGITS + 1], tbuf[R][POL_BUCKETS];
-    __shared__ int32_t abuf[R][POL_BUCKETS];
-    const int r = lane / LPR, part = lane % LPR;
-    const int64_t rr = row0 + r;
-    const bool live = rr < a.rows;
-    const bool stochastic = a.stochastic != 0;
-    const float *lg = tile[r];
-    // bucket maxima (every lane, compile-time indices)
-    float mx[POL_BUCKETS];
-#pragma unroll
-    for (int b = 0; b < POL_BUCKETS; b++) {
-        const int o = pol_bucket_off(b), nb = pol_bucket(b);
-        float m = lg[o];
-        for (int i = 1; i < nb; i++) m = lg[o + i] > m ? lg[o + i] : m;
-        mx[b] = m;
-    }
-#pragma unroll
-    for (int j = 0; j < PPL; j++) {
-        const int pr = part + LPR * j;
-        if (pr < PAIRS) {
-            uint32_t b0 = 0, b1 = 0;
-            if (stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
-#pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int i = 2 * pr + h;
-                if (i < POL_LOGITS) {
-                    const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
-                    float m = mx[0];
-#pragma unroll
-                    for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
-                    const float x = lg[i];
-                    // pol_gumbel's value for logit i (its threefry word h)
-                    const float g = stochastic ? x + (-pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)))) : x;
-                    gbuf[r][i] = g;
-                    ebuf[r][i] = pol_expf(x - m);
-                }
-            }
-        }
-    }
-    pol_wave_sync();
-#pragma unroll
-    for (int j = 0; j < BPL; j++) {
-        const int b = part + LPR * j;
-        if (b < POL_BUCKETS) {
-            const int o = pol_bucket_off(b), nb = pol_bucket(b);
-            float best = gbuf[r][o], s = ebuf[r][o];
-            int act = 0;
-#pragma unroll
-            for (int i = 1; i < 8; i++) {
-                if (i < nb) {
-                    const float g = gbuf[r][o + i];
-                    if (g > best) { best = g; act = i; }  // first maximum
-                    s = s + ebuf[r][o + i];
-                }
-            }
-            float m = mx[0];
-#pragma unroll
-            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
-            const float lse = m + pol_logf(s);
-            abuf[r][b] = act;
-            tbuf[r][b] = lg[o + act] - lse;
-        }
-    }
-    pol_wave_sync();
-    if (part == 0 && live) {
-        float term[POL_BUCKETS];
-        int32_t act[POL_BUCKETS];
-#pragma unroll
-        for (int b = 0; b < POL_BUCKETS; b++) { term[b] = tbuf[r][b]; act[b] = abuf[r][b]; }
-        const float lp = pol_logp_sum(term);
-        if (a.actions) {
-            int32_t *d = a.actions + rr * a.act_stride;
-#pragma unroll
-            for (int b = 0; b < 6; b++) d[b] = act[b];
-        }
-        if (a.act_out) {
-            int2 *d = (int2 *)(a.act_out + rr * 6);
-            d[0] = make_int2(act[0], act[1]);
-            d[1] = make_int2(act[2], act[3]);
-            d[2] = make_int2(act[4], act[5]);
-        }
-        if (a.log_prob) a.log_prob[rr] = lp;
-        if (a.value) a.value[rr] = lg[POL_LOGITS];
-        if (a.rew_out) {  // the previous step's outcome of this row (buffer.rewards / not_dones)
-            a.rew_out[rr] = a.rew_src[rr * a.rd_stride];
-            a.done_out[rr] = a.done_src[rr * a.rd_stride];
-        }
-    }
-}
 
 // diagnostics (PolicyArgs::diag_ts): the clock at phase boundaries of the
 // wave's first tile -- 0 start, 1 weights loaded, 2 rows loaded, 3 layer 1,
@@ -188,8 +37,8 @@ __device__ __forceinline__ void pol_trace(const PolicyArgs &a, bool first, int p
 template <int MT>
 __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
 {
-    pol_trace(a, true, 0, false);
     // MT: 16-row M-tiles per tile
+    pol_trace(a, true, 0, false);
     __shared__ __attribute__((aligned(16))) float norm[2][POL_IN];
     __shared__ float tile[16 * MT][33];
     const int lane = threadIdx.x, c = lane & 15, q = lane >> 4;
@@ -199,27 +48,9 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
         norm[1][k] = W.obs_inv[k];
     }
     // B operands, loaded once per (persistent) wave
-    float w1[2][32], w2[2][8], wh[2][8];
-#pragma unroll
-    for (int t = 0; t < 2; t++) {
-        const float4 *src = (const float4 *)(W.w1 + (16 * t + c) * POL_IN + 32 * q);
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            const float4 x = src[v];
-            w1[t][4 * v] = x.x; w1[t][4 * v + 1] = x.y; w1[t][4 * v + 2] = x.z; w1[t][4 * v + 3] = x.w;
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            w2[t][j] = W.w2[(16 * t + c) * POL_HID + 8 * q + j];
-            wh[t][j] = W.head_w[(16 * t + c) * POL_HID + 8 * q + j];
-        }
-    }
-    const float b1_0 = W.b1[c], b1_1 = W.b1[c + 16], l1w0 = W.ln1_w[c], l1w1 = W.ln1_w[c + 16];
-    const float l1b0 = W.ln1_b[c], l1b1 = W.ln1_b[c + 16];
-    const float b2_0 = W.b2[c], b2_1 = W.b2[c + 16], l2w0 = W.ln2_w[c], l2w1 = W.ln2_w[c + 16];
-    const float l2b0 = W.ln2_b[c], l2b1 = W.ln2_b[c + 16];
-    const float bh0 = W.head_b[c], bh1 = W.head_b[c + 16];
-    __syncthreads();
+    PolicyRegs R;
+    load_policy_regs(R, W, c, q);
+    pol_wave_sync();
     pol_trace(a, true, 1, true);
 
     const int64_t tiles = (a.rows + 16 * MT - 1) / (16 * MT);
@@ -250,70 +81,12 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
             }
         }
         pol_trace(a, first, 2, true);
-        // layer 1 (two independent accumulators per M-tile keep the MFMA pipe full)
-        float nm[32], ni[32];
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            const float4 a4 = *(const float4 *)&norm[0][32 * q + 4 * v];
-            const float4 b4 = *(const float4 *)&norm[1][32 * q + 4 * v];
-            nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
-            ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
-        }
-#pragma unroll
-        for (int m = 0; m < MT; m++) {
-            // the VALU normalisation as one block, then the MFMA chain back to back
-            // (interleaved, every MFMA waits out a VALU-write hazard)
-#pragma unroll
-            for (int j = 0; j < 32; j++) x[m][j] = pol_clamp((x[m][j] - nm[j]) * ni[j]);
-            __builtin_amdgcn_sched_barrier(0);
-            f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < 32; j++) {
-                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], w1[0][j], a0, 0, 0, 0);
-                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], w1[1][j], a1, 0, 0, 0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            ln_relu_to_tile(a0, a1, b1_0, b1_1, l1w0, l1w1, l1b0, l1b1, tile + 16 * m, c, q);
-        }
-        __syncthreads();
-        pol_trace(a, first, 3, false);
-        // layer 2 and heads, per M-tile through its 16 rows of the tile
-#pragma unroll
-        for (int m = 0; m < MT; m++) {
-            float (*tm)[33] = tile + 16 * m;
-            float h[8];
-#pragma unroll
-            for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
-            __syncthreads();
-            f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w2[0][j], a0, 0, 0, 0);
-                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w2[1][j], a1, 0, 0, 0);
-            }
-            ln_relu_to_tile(a0, a1, b2_0, b2_1, l2w0, l2w1, l2b0, l2b1, tm, c, q);
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
-            __syncthreads();
-            a0 = f32x4{0.f, 0.f, 0.f, 0.f};
-            a1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int j = 0; j < 8; j++) {
-                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], wh[0][j], a0, 0, 0, 0);
-                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], wh[1][j], a1, 0, 0, 0);
-            }
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                tm[4 * q + i][c] = a0[i] + bh0;
-                tm[4 * q + i][c + 16] = a1[i] + bh1;
-            }
-        }
-        __syncthreads();
+        policy_layers<MT>(x, R, norm, tile, c, q);
         pol_trace(a, first, 4, false);
         if constexpr (16 * MT < 64) {
-            bucket_pass_spread<MT>(a, tile, row0, lane);
-            __syncthreads();
+            __shared__ BucketLds<MT> bl;
+            bucket_pass_spread<MT>(a, tile, row0, lane, bl);
+            pol_wave_sync();
             pol_trace(a, first, 5, false);
             continue;
         }
@@ -344,7 +117,8 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
                 a.done_out[rr] = a.done_src[rr * a.rd_stride];
             }
         }
-        __syncthreads();
+        pol_wave_sync();
+        pol_trace(a, first, 5, false);
     }
 }
 

@@ -1,0 +1,285 @@
+// bb_policy_dev.h -- device building blocks of the policy network on gfx950
+// (bb_policy.h has the row math and the reference lines): the MFMA layers of
+// one 16 MT-row tile and the bucket pass, shared by k_policy (bb_policy.hip)
+// and the fused PPO rollout kernel (bb_kernels.hip k_rollout_policy), so that
+// both compute the very same bits.
+//
+// The three matrix products run on v_mfma_f32_16x16x4_f32 (exact f32, a
+// k-ordered fmaf chain):
+//   layer 1  [16 x 128] x [128 x 32]: lane (r = l & 15, q = l >> 4) feeds
+//            A = x[r][32q + j] and B = W1[n][32q + j] for j = 0..31 (32
+//            contiguous floats of its row; its 64 weights in registers);
+//   layer 2 / heads  [16 x 32] x [32 x 32]: k = 8q + j, the hidden tile
+//            transposed through a 16 x 33 LDS tile.
+// The C/D layout (col = l & 15, row = 4q + i) puts a row's 32 outputs on the 16
+// lanes of one quarter-wave: LayerNorm is a 4-step xor butterfly there.
+// Synchronisation inside a tile is wave-local (pol_wave_sync): the LDS words a
+// wave exchanges are its own, so the pieces run in multi-wave workgroups too.
+#pragma once
+#include <hip/hip_runtime.h>
+#include "bb_policy.h"
+
+namespace bb {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Ordering of LDS words written and read by different lanes of the wave.
+__device__ __forceinline__ void pol_wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+
+
+// Sum over the 16 lanes of a DPP row, the same tree as bb_policy.h pol_sum32's
+// xor butterfly (partners 1, 2, then the other quad / half: once a quad holds
+// equal values any cross-quad partner gives the same bits): four DPP adds.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x)
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quarter_sum(float t)
+{
+    t = t + dpp_f<0xB1>(t);   // quad_perm [1,0,3,2]: xor 1
+    t = t + dpp_f<0x4E>(t);   // quad_perm [2,3,0,1]: xor 2
+    t = t + dpp_f<0x141>(t);  // row_half_mirror: the other quad of the 8
+    t = t + dpp_f<0x140>(t);  // row_mirror: the other 8 of the 16
+    return t;
+}
+
+// LayerNorm + ReLU of the 4 rows a lane holds (cols c and c + 16), then the
+// result into the LDS tile [row][col].
+__device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0, float bias1, float w0, float w1,
+                                                float lb0, float lb1, float (*tile)[33], int c, int q)
+{
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
+        const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
+        const float d0 = h0 - mean, d1 = h1 - mean;
+        const float var = quarter_sum((d0 * d0) + (d1 * d1)) * (1.0f / 32.0f);
+        const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
+        tile[4 * q + i][c] = pol_relu(((d0 * inv) * w0) + lb0);
+        tile[4 * q + i][c + 16] = pol_relu(((d1 * inv) * w1) + lb1);
+    }
+}
+
+// Bucket pass of a tile of R = 16 MT < 64 rows: LPR = 64 / R lanes per row,
+// every step the same instructions on different data (no divergent roles):
+//   A  lane part p: the Gumbel noise of logit pairs p, p + LPR, ... (one
+//      threefry call per pair) and, per logit, g = logit + noise and
+//      e = exp(logit - bucket max), into LDS;
+//   B  lane part p: buckets p, p + LPR, ...: first maximum of g, sum of e in
+//      logit order, logit - logsumexp, into LDS;
+//   C  lane part 0: the six terms summed in bucket order, the outputs.
+// Every value is the one pol_bucket_term / pol_select computes (same
+// operations on the same inputs), so rows are bit-identical to MT = 4's.
+// The bucket pass's LDS exchange of one wave (16 MT rows).
+template <int MT>
+struct BucketLds {
+    float g[16 * MT][POL_LOGITS + 1], e[16 * MT][POL_LOGITS + 1], t[16 * MT][POL_BUCKETS];
+    int32_t a[16 * MT][POL_BUCKETS];
+};
+
+// act_local (optional): row r's six actions also into act_local[r] (LDS).
+template <int MT>
+__device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
+                                                   BucketLds<MT> &buf, int32_t (*act_local)[6] = nullptr)
+{
+    constexpr int R = 16 * MT, LPR = 64 / R;
+    constexpr int PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    float (*gbuf)[POL_LOGITS + 1] = buf.g, (*ebuf)[POL_LOGITS + 1] = buf.e, (*tbuf)[POL_BUCKETS] = buf.t;
+    int32_t (*abuf)[POL_BUCKETS] = buf.a;
+    const int r = lane / LPR, part = lane % LPR;
+    const int64_t rr = row0 + r;
+    const bool live = rr < a.rows;
+    const bool stochastic = a.stochastic != 0;
+    const float *lg = tile[r];
+    // bucket maxima (every lane, compile-time indices)
+    float mx[POL_BUCKETS];
+#pragma unroll
+    for (int b = 0; b < POL_BUCKETS; b++) {
+        const int o = pol_bucket_off(b), nb = pol_bucket(b);
+        float m = lg[o];
+        for (int i = 1; i < nb; i++) m = lg[o + i] > m ? lg[o + i] : m;
+        mx[b] = m;
+    }
+#pragma unroll
+    for (int j = 0; j < PPL; j++) {
+        const int pr = part + LPR * j;
+        if (pr < PAIRS) {
+            uint32_t b0 = 0, b1 = 0;
+            if (stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int i = 2 * pr + h;
+                if (i < POL_LOGITS) {
+                    const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
+                    float m = mx[0];
+#pragma unroll
+                    for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
+                    const float x = lg[i];
+                    // pol_gumbel's value for logit i (its threefry word h)
+                    const float g = stochastic ? x + (-pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)))) : x;
+                    gbuf[r][i] = g;
+                    ebuf[r][i] = pol_expf(x - m);
+                }
+            }
+        }
+    }
+    pol_wave_sync();
+#pragma unroll
+    for (int j = 0; j < BPL; j++) {
+        const int b = part + LPR * j;
+        if (b < POL_BUCKETS) {
+            const int o = pol_bucket_off(b), nb = pol_bucket(b);
+            float best = gbuf[r][o], s = ebuf[r][o];
+            int act = 0;
+#pragma unroll
+            for (int i = 1; i < 8; i++) {
+                if (i < nb) {
+                    const float g = gbuf[r][o + i];
+                    if (g > best) { best = g; act = i; }  // first maximum
+                    s = s + ebuf[r][o + i];
+                }
+            }
+            float m = mx[0];
+#pragma unroll
+            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
+            const float lse = m + pol_logf(s);
+            abuf[r][b] = act;
+            tbuf[r][b] = lg[o + act] - lse;
+        }
+    }
+    pol_wave_sync();
+    if (part == 0 && live) {
+        float term[POL_BUCKETS];
+        int32_t act[POL_BUCKETS];
+#pragma unroll
+        for (int b = 0; b < POL_BUCKETS; b++) { term[b] = tbuf[r][b]; act[b] = abuf[r][b]; }
+        const float lp = pol_logp_sum(term);
+        if (act_local)
+#pragma unroll
+            for (int b = 0; b < 6; b++) act_local[r][b] = act[b];
+        if (a.actions) {
+            int32_t *d = a.actions + rr * a.act_stride;
+#pragma unroll
+            for (int b = 0; b < 6; b++) d[b] = act[b];
+        }
+        if (a.act_out) {
+            int2 *d = (int2 *)(a.act_out + rr * 6);
+            d[0] = make_int2(act[0], act[1]);
+            d[1] = make_int2(act[2], act[3]);
+            d[2] = make_int2(act[4], act[5]);
+        }
+        if (a.log_prob) a.log_prob[rr] = lp;
+        if (a.value) a.value[rr] = lg[POL_LOGITS];
+        if (a.rew_out) {  // the previous step's outcome of this row (buffer.rewards / not_dones)
+            a.rew_out[rr] = a.rew_src[rr * a.rd_stride];
+            a.done_out[rr] = a.done_src[rr * a.rd_stride];
+        }
+    }
+}
+
+// The B operands and the per-column constants of one lane, loaded once per
+// wave and kept in registers for every tile it processes.
+struct PolicyRegs {
+    float w1[2][32], w2[2][8], wh[2][8];
+    float b1_0, b1_1, l1w0, l1w1, l1b0, l1b1, b2_0, b2_1, l2w0, l2w1, l2b0, l2b1, bh0, bh1;
+};
+
+__device__ __forceinline__ void load_policy_regs(PolicyRegs &R, const PolicyWeights &W, int c, int q)
+{
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+        const float4 *src = (const float4 *)(W.w1 + (16 * t + c) * POL_IN + 32 * q);
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float4 x = src[v];
+            R.w1[t][4 * v] = x.x; R.w1[t][4 * v + 1] = x.y; R.w1[t][4 * v + 2] = x.z; R.w1[t][4 * v + 3] = x.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            R.w2[t][j] = W.w2[(16 * t + c) * POL_HID + 8 * q + j];
+            R.wh[t][j] = W.head_w[(16 * t + c) * POL_HID + 8 * q + j];
+        }
+    }
+    R.b1_0 = W.b1[c]; R.b1_1 = W.b1[c + 16]; R.l1w0 = W.ln1_w[c]; R.l1w1 = W.ln1_w[c + 16];
+    R.l1b0 = W.ln1_b[c]; R.l1b1 = W.ln1_b[c + 16];
+    R.b2_0 = W.b2[c]; R.b2_1 = W.b2[c + 16]; R.l2w0 = W.ln2_w[c]; R.l2w1 = W.ln2_w[c + 16];
+    R.l2b0 = W.ln2_b[c]; R.l2b1 = W.ln2_b[c + 16];
+    R.bh0 = W.head_b[c]; R.bh1 = W.head_b[c + 16];
+}
+
+// The network on one tile of 16 MT rows: x[m][j] = observation float 32q + j
+// of row 16m + c (lane (c, q)); norm = {mean, rsqrt(var + eps)} in LDS.
+// Leaves each row's 19 logits and value (column 19) in tile[row][0..19].
+template <int MT>
+__device__ __forceinline__ void policy_layers(float (&x)[MT][32], const PolicyRegs &R, const float (*norm)[POL_IN],
+                                              float (*tile)[33], int c, int q)
+{
+    // layer 1 (two independent accumulators per M-tile keep the MFMA pipe full)
+    float nm[32], ni[32];
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        const float4 a4 = *(const float4 *)&norm[0][32 * q + 4 * v];
+        const float4 b4 = *(const float4 *)&norm[1][32 * q + 4 * v];
+        nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
+        ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
+    }
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+        // the VALU normalisation as one block, then the MFMA chain back to back
+        // (interleaved, every MFMA waits out a VALU-write hazard)
+#pragma unroll
+        for (int j = 0; j < 32; j++) x[m][j] = pol_clamp((x[m][j] - nm[j]) * ni[j]);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 32; j++) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], R.w1[0][j], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], R.w1[1][j], a1, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        ln_relu_to_tile(a0, a1, R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1, tile + 16 * m, c, q);
+    }
+    pol_wave_sync();
+    // layer 2 and heads, per M-tile through its 16 rows of the tile
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+        float (*tm)[33] = tile + 16 * m;
+        float h[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
+        pol_wave_sync();
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[0][j], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[1][j], a1, 0, 0, 0);
+        }
+        ln_relu_to_tile(a0, a1, R.b2_0, R.b2_1, R.l2w0, R.l2w1, R.l2b0, R.l2b1, tm, c, q);
+        pol_wave_sync();
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
+        pol_wave_sync();
+        a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+        a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[0][j], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[1][j], a1, 0, 0, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            tm[4 * q + i][c] = a0[i] + R.bh0;
+            tm[4 * q + i][c + 16] = a1[i] + R.bh1;
+        }
+    }
+    pol_wave_sync();
+}
+
+}  // namespace bb

@@ -192,14 +192,16 @@ class FusedPolicy:
                 "next_value": torch.zeros((W,), dtype=f32, device=dev)}
 
     def rollout(self, sim, n: int, buffers: dict, trainee: int = 0, stochastic: bool = True, seed: int = 0,
-                step0: int = 0, opponent: "FusedPolicy" = None, time_kernels: bool = False):
+                step0: int = 0, opponent: "FusedPolicy" = None, per_step: bool = False, time_kernels: bool = False):
         """PPO's rollout loop (scripts/ppo.py:61-141) on the device, bb_rollout_policy:
         n x (this policy acts for agent `trainee` of every world; [the frozen
         `opponent` acts for the other agent, env.py:127-143]; step) with the
         buffer stores of ppo.py:129-134 and next_value = evaluate(last obs).
         Bit for bit n x (act(); [opponent.act()]; sim.step()) with the same reads.
-        Any entry of `buffers` may be None (not recorded).  Returns the elapsed
-        device ms when time_kernels."""
+        Any entry of `buffers` may be None (not recorded).  On gfx950 (2 agents,
+        no opponent, up to 8 192 worlds) one fused launch runs every step;
+        per_step=True forces a policy launch + a step launch per step.  Returns
+        the elapsed device ms when time_kernels."""
         W = sim.num_worlds
         shapes = {"obs": ((n, W, IN), torch.float32), "actions": ((n, W, 6), torch.int32),
                   "log_prob": ((n, W), torch.float32), "value": ((n, W), torch.float32),
@@ -223,5 +225,6 @@ class FusedPolicy:
         _lib.check(_lib.load().bb_rollout_policy(
             sim._h, ctypes.byref(self._w), ctypes.byref(opponent._w) if opponent is not None else None, int(n),
             int(trainee), 1 if stochastic else 0, int(seed) & 0xFFFFFFFF, int(step0) & 0xFFFFFFFF,
-            ctypes.byref(out), sim._stream(), ctypes.byref(ms) if time_kernels else None), "rollout_policy")
+            ctypes.byref(out), _lib.ROLLOUT_PER_STEP if per_step else 0, sim._stream(),
+            ctypes.byref(ms) if time_kernels else None), "rollout_policy")
         return ms.value if time_kernels else None

@@ -104,6 +104,26 @@ def test_gpu_policy_rollout_equals_the_ppo_loop(native_lib, trainee, stochastic,
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("W,n,trainee,stochastic", [(8192, 32, 0, True), (1000, 20, 1, False), (64, 3, 0, True)])
+def test_gpu_fused_policy_rollout_equals_per_step_launches(native_lib, W, n, trainee, stochastic):
+    """The fused PPO rollout kernel (one launch, k_rollout_policy) == a policy
+    launch + a step launch per step, every output and every column, bit for bit
+    (a partial last workgroup included: W = 1000, 64)."""
+    assert torch.cuda.is_available()
+    sims = [make_sim(ExecMode.CUDA, W, per_world_rng=True) for _ in range(2)]
+    for s in sims:
+        s.step_n(9, random_actions=True, action_seed=321, step0=0)
+    pol = FusedPolicy.from_agent(make_agent(5).cuda())
+    bufs = [pol.rollout_buffers(s, n) for s in sims]
+    pol.rollout(sims[0], n, bufs[0], trainee=trainee, stochastic=stochastic, seed=7, step0=3)
+    pol.rollout(sims[1], n, bufs[1], trainee=trainee, stochastic=stochastic, seed=7, step0=3, per_step=True)
+    torch.cuda.synchronize()
+    assert_same(bufs[0], bufs[1])
+    for name in sims[0]._views:
+        assert torch.equal(sims[0]._views[name], sims[1]._views[name]), name
+
+
+@pytest.mark.gpu
 def test_gpu_policy_rollout_equals_host_executor(native_lib):
     """Device rollout == host-executor rollout (policy and step), bit for bit."""
     assert torch.cuda.is_available()

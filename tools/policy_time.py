@@ -50,11 +50,10 @@ def main():
             t = t[t[:, 0] > 0]
             t -= t[:, 0].min()
             pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
-            names = ["weights", "rows", "layer1", "layer2+heads", "buckets"]
             print(f"trace rows {obs.shape[0]} stochastic={stoch} waves {len(t)} (10 ns ticks) start {pct(t[:, 0])} "
                   f"end {pct(t[:, 5])}", flush=True)
-            for i, n in enumerate(names):
-                print(f"  {n:14s} {pct(t[:, i + 1] - t[:, i])}", flush=True)
+            for n, i, j in (("weights", 0, 1), ("rows", 1, 2), ("layers", 2, 4), ("buckets", 4, 5)):
+                print(f"  {n:14s} {pct(t[:, j] - t[:, i])}", flush=True)
     for label, obs in cases:
         rows = obs.shape[0]
         act = torch.empty((rows, 6), dtype=torch.int32, device="cuda")
