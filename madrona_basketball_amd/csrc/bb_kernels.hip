@@ -88,6 +88,16 @@ __device__ __forceinline__ const double *erf_table_lds()
     return tab;
 }
 
+// Ordering of LDS words written and read by different lanes of one wave (a
+// wave's LDS operations execute in order): keeps the compiler from moving
+// them across each other.
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int N>
 struct ObsTile {
     static constexpr int QW = (obs_used(N) + 3) / 4;  // float4 pieces of a used row
@@ -494,6 +504,33 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
 }
 
 // One lane per agent: lane = (w - w0) * N + k.
+// k_step's copy of the erf Taylor table in LDS (BB_STEP_ERF_LDS, off): the
+// table's loads issued ahead of the state's, its LDS writes before the
+// systems.  Measured slower at every size (profiles/r03/i_erf_lds_ab.txt:
+// 8 192 worlds 11.65 -> 12.33 us, 65 536 21.9 -> 23.3, 262 144 74.6 -> 78.1):
+// the copy lengthens the load phase (0.96 -> 1.74 us at 8 192) while the
+// coefficient reads it removes are L2 hits off the critical path.
+#ifndef BB_STEP_ERF_LDS
+#define BB_STEP_ERF_LDS 0
+#endif
+constexpr int ERF_PER_LANE = (ERF_WORDS + WAVE - 1) / WAVE;
+__device__ __forceinline__ void erf_table_fetch(double (&e)[ERF_PER_LANE], int lane)
+{
+#pragma unroll
+    for (int j = 0; j < ERF_PER_LANE; j++) {
+        const int i = j * WAVE + lane;
+        e[j] = i < ERF_WORDS ? (&bbm::ERF_TAYLOR[0][0])[i] : 0.0;
+    }
+}
+__device__ __forceinline__ void erf_table_put(double *tab, const double (&e)[ERF_PER_LANE], int lane)
+{
+#pragma unroll
+    for (int j = 0; j < ERF_PER_LANE; j++) {
+        const int i = j * WAVE + lane;
+        if (i < ERF_WORDS) tab[i] = e[j];
+    }
+}
+
 template <int N, int MODE, bool LINES>
 __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 {
@@ -509,6 +546,9 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;  // the world with this lane's agent in slot 0
     trace_point<MODE>(p, 0);
+    double erf_words[ERF_PER_LANE];
+    __shared__ double erf_tab[BB_STEP_ERF_LDS ? ERF_WORDS : 1];
+    if constexpr (BB_STEP_ERF_LDS) erf_table_fetch(erf_words, lane);
     // The event-only words as loaded (store only on change, see Orig) wait
     // in the observation tile, which is free until the observation pass:
     // registers stay with the systems.
@@ -523,6 +563,13 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
             x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
             park_words(tile, lane, x);
         }
+    }
+    if constexpr (BB_STEP_ERF_LDS) {
+        erf_table_put(erf_tab, erf_words, lane);
+        wave_sync();
+        c.erf_tab = erf_tab;
+    }
+    if (active) {
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, p.diag_dup);
         else if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) step_world_pre_obs(s, c, ag);
     }
@@ -581,15 +628,6 @@ struct Wide {
 #endif
 constexpr uint32_t SHOT_PCT_UNSET = 0x7FC0BEEFu;  // a NaN the step never computes
 
-// Ordering of LDS words written and read by different lanes of one wave (a
-// wave's LDS operations execute in order): keeps the compiler from moving
-// them across each other.
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 template <int N, int PHASE>
 __device__ __forceinline__ void wide_obs_pass(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,

@@ -126,3 +126,51 @@ def test_sharded_rollouts_equal_single_process():
     full.rollout(acts, buf["obs"], buf["reward"], buf["done"])
     for g, key in zip(got, ("obs", "reward", "done")):
         assert np.array_equal(g.view(np.uint32), buf[key].numpy().view(np.uint32)), key
+
+
+def _gather_worker(rank, world, port, W, steps, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    from madrona_basketball_amd.sharding import gather_observations, shard
+    off, n = shard(W, rank, world)
+    sim = make_sim(ExecMode.CPU, n, per_world_rng=True, world_offset=off)
+    sim.step_n(steps, random_actions=True, action_seed=5)
+    full = gather_observations(sim)
+    one = gather_observations(sim, agent=1)
+    if rank == 0:
+        q.put((full.numpy().copy(), one.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_observations_two_ranks():
+    """The optional observation all-gather of SURVEY 8(e) (madrona_basketball_amd.sharding):
+    two shards' rows gathered == the unsharded simulator's rows, whole and per agent."""
+    from tests.helpers import make_sim
+    from madrona_basketball_amd import ExecMode
+    W, steps, world = 256, 40, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_gather_worker, args=(r, world, port, W, steps, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, one = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = make_sim(ExecMode.CPU, W, per_world_rng=True)
+    ref.step_n(steps, random_actions=True, action_seed=5)
+    obs = ref.observations_tensor().to_torch().numpy()
+    assert np.array_equal(full.view(np.uint32), obs.view(np.uint32))
+    assert np.array_equal(one.view(np.uint32), obs[:, 1].copy().view(np.uint32))
+
+
+def test_shard_ranges():
+    from madrona_basketball_amd.sharding import shard
+    assert [shard(262144, r, 8) for r in (0, 7)] == [(0, 32768), (229376, 32768)]
+    with pytest.raises(ValueError):
+        shard(1000, 0, 3)
