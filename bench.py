@@ -295,8 +295,17 @@ def main():
         barrier()
         e2e_s = max_over_ranks(e2e_s)
         del trainee
+        # the same loop with SimpleGridworldSimulator.step() alone (Python + ctypes
+        # + the launch, no torch kernels): the per-call cost of the binding
+        barrier()
+        t0 = time.perf_counter()
+        for t in range(args.steps):
+            sim.step()
+        sync()
+        step_only_s = max_over_ranks(time.perf_counter() - t0)
         e2e = {"value": W * world_size * args.steps / e2e_s, "unit": "env-steps/s",
                "ms_per_step": e2e_s * 1e3 / args.steps,
+               "step_call_only_us": step_only_s * 1e6 / args.steps,
                "harness": "scripts/run.py loop over env.step(): int64 trainee actions -> actions[:, 0] "
                           "(env.py:147), SimpleGridworldSimulator.step() via ctypes, obs/reward/done "
                           "[:, 0].clone() (env.py:167-170); agent 1 acts through the hard-coded defence"}

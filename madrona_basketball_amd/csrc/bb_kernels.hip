@@ -38,7 +38,15 @@ constexpr int WAVE = 64;
 // from the XCD's L2, so no dirty row lines are left for the end-of-kernel
 // write-back).
 #ifndef BB_STEP_AUX
-#define BB_STEP_AUX -1  // k_step, rows cache-resident
+// k_step, rows cache-resident: write-through (sc1), which leaves the kernel
+// fewer dirty L2 lines to settle at its end -- measured 8 192 worlds 11.65 ->
+// 11.13 us, 16 384 12.93 -> 12.15, 32 768 15.7 -> 15.4 (profiles/r03/
+// k_store_policy_small_ab.txt), 65 536 equal (r02 o_store_policy_ab.txt);
+// nt is slower at every cache-resident size.
+#define BB_STEP_AUX 16
+#endif
+#ifndef BB_COL_AUX
+#define BB_COL_AUX -1  // k_step<2>, state column stores (vector chunks)
 #endif
 #ifndef BB_LINES_AUX
 #define BB_LINES_AUX 2  // k_step, state beyond the Infinity Cache
@@ -581,11 +589,11 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
         // observation row is built
         if constexpr (MODE != MODE_IO && MODE != MODE_IO_OBS) sys_reward_agent(v, 0, AGENT0_ID + k);
         const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
-        store_world_agent(v, p, w * N + k, 0, &x.agent);
+        store_world_agent<N, BB_COL_AUX>(v, p, w * N + k, 0, &x.agent);
         if (k == 0) {
             Orig<N> o;
             set_world_orig(o, x.world);
-            store_world_shared(s, p, w, &o);
+            store_world_shared<N, BB_COL_AUX>(s, p, w, &o);
         }
     }
     trace_point<MODE>(p, 8);
@@ -993,14 +1001,21 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
 //      into X (and on the last step every row into the sim's tensor);  -> barrier
 // then P's value pass over the final X gives next_value (ppo.py:136-137), and S
 // stores every column of the worlds (the state after step K-1).
-constexpr int PPO_PWAVES = 2;
+// Policy waves: two per 16-row M-tile, wave h of a pair running output columns
+// 16h..16h+15 of every product and the LayerNorm of half the rows
+// (policy_layers_half: PPO_LAYER_BARS workgroup barriers per pass, which the
+// sim wave passes while it waits), then the bucket pass of 8 rows.
+constexpr int PPO_PWAVES = 4;
+constexpr int PPO_LAYER_BARS = 5;
 constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
 struct PpoLds {
     float x[32][PPO_XS];
     int32_t act[32][6];
     float norm[2][POL_IN];
-    float ptile[PPO_PWAVES][16][33];
-    BucketLds<1> bucket[PPO_PWAVES];
+    float ptile[2][16][33];   // hidden activations of each M-tile
+    float ltile[2][16][33];   // logits + value of each M-tile
+    HalfExchange ex[2];
+    BucketLds<8> bucket[PPO_PWAVES];
     double erf[ERF_WORDS];
 };
 
@@ -1070,6 +1085,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         Ctx c = make_ctx(p, w_t, k == 0);
         c.erf_tab = L.erf;
         const LaneAgents<N, MODE_FULL> ag{k, &p};
+        for (int b = 0; b < PPO_LAYER_BARS; b++) __syncthreads();  // (the policy pass's own barriers)
         __syncthreads();  // the policy's actions are in LDS
         ppo_trace(r, t, 0);
         int32_t ib = -1;
@@ -1132,30 +1148,32 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         store_world_agent(v, p, w_s * N + k, 0);
         if (k == 0) store_world_shared(v, p, w_s);
     }
+    for (int b = 0; b < PPO_LAYER_BARS; b++) __syncthreads();  // (the next-value pass's barriers)
 }
 
 __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
 {
     const int lane = threadIdx.x % WAVE, c = lane & 15, q = lane >> 4;
     const int64_t W = p.num_worlds;
-    const int r0 = 16 * pw;                                   // first X row of this wave
+    const int m = pw >> 1, h = pw & 1;                        // M-tile, column half
+    const int r0 = 16 * m;                                    // first X row of the M-tile
     const int64_t row0 = (int64_t)blockIdx.x * 32 + r0;       // its first world
-    float (*tile)[33] = L.ptile[pw];
-    // network constants: norm by the lanes of both policy waves, B operands per lane
+    const int rh = 8 * h;                                     // this wave's 8 rows of the tile (bucket pass, records)
+    // network constants: norm by the lanes of the policy waves, B operands per lane
     for (int k = pw * WAVE + lane; k < POL_IN; k += PPO_PWAVES * WAVE) {
         L.norm[0][k] = r.w.obs_mean[k];
         L.norm[1][k] = r.w.obs_inv[k];
     }
     PolicyRegs R;
     load_policy_regs(R, r.w, c, q);
-    // X for step 0: the trainee rows of the sim's observation tensor (and a
-    // zero tail, which emit never writes)
-    for (int i = lane; i < 16 * 32; i += WAVE) {
-        const int rr = i / 32, qq = i % 32;
-        const int64_t wg = row0 + rr;
+    // X for step 0: the trainee rows of the sim's observation tensor (with
+    // their zero tail, which emit never writes)
+    for (int i = lane; i < 8 * 32; i += WAVE) {
+        const int rr = r0 + rh + i / 32, qq = i % 32;
+        const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
         float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (wg < W) v4 = *(const float4 *)(p.c.obs + (wg * 2 + r.trainee) * (int64_t)obs_width(2) + 4 * qq);
-        *(float4 *)&L.x[r0 + rr][4 * qq] = v4;
+        *(float4 *)&L.x[rr][4 * qq] = v4;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     __syncthreads();  // setup
@@ -1163,35 +1181,35 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     a.rows = W;
     a.stochastic = r.stochastic;
     a.seed = r.seed;
+    auto bar = [] { __syncthreads(); };
     for (int t = 0; t <= r.steps; t++) {
         const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
-        if (!final_pass && r.obs_out) {  // buffer.obs[t] = X
-            for (int i = lane; i < 16 * 32; i += WAVE) {
-                const int rr = i / 32, qq = i % 32;
-                const int64_t wg = row0 + rr;
-                if (wg < W) *(float4 *)(r.obs_out + ((int64_t)t * W + wg) * POL_IN + 4 * qq) = *(const float4 *)&L.x[r0 + rr][4 * qq];
+        if (!final_pass && r.obs_out) {  // buffer.obs[t] = X, this wave's 8 rows
+            for (int i = lane; i < 8 * 32; i += WAVE) {
+                const int rr = r0 + rh + i / 32, qq = i % 32;
+                const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
+                if (wg < W) *(float4 *)(r.obs_out + ((int64_t)t * W + wg) * POL_IN + 4 * qq) = *(const float4 *)&L.x[rr][4 * qq];
             }
         }
-        float x[1][32];
+        float x[32];
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             const float4 o = *(const float4 *)&L.x[r0 + c][32 * q + 4 * v];
-            x[0][4 * v] = o.x; x[0][4 * v + 1] = o.y; x[0][4 * v + 2] = o.z; x[0][4 * v + 3] = o.w;
+            x[4 * v] = o.x; x[4 * v + 1] = o.y; x[4 * v + 2] = o.z; x[4 * v + 3] = o.w;
         }
-        policy_layers<1>(x, R, L.norm, tile, c, q);
+        policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, bar);
         a.step = r.step0 + (uint32_t)t;
         if (!final_pass) {
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
-            bucket_pass_spread<1>(a, tile, row0, lane, L.bucket[pw], L.act + r0);
+            bucket_pass_spread<8>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh);
             pol_wave_sync();
             if (pw == 0) ppo_trace(r, t, 3);
             __syncthreads();  // actions in LDS
             __syncthreads();  // X holds the observations after step t
-        } else if (r.next_value) {
-            const int rr = lane >> 2;
-            if ((lane & 3) == 0 && row0 + rr < W) r.next_value[row0 + rr] = tile[rr][POL_LOGITS];
+        } else if (r.next_value && lane < 8 && row0 + rh + lane < W) {
+            r.next_value[row0 + rh + lane] = L.ltile[m][rh + lane][POL_LOGITS];
         }
     }
 }
@@ -1348,15 +1366,27 @@ struct DppAgents {
     static constexpr bool value = BB_DPP_AGENTS && N == 4 && XW < INTRINSIC;
 };
 
+// The observation pass writes the row-source table for OBS_PARTS groups of
+// the wave's worlds in turn (a group's rows emitted before the next group's
+// sources overlay them), so the table needs room for WPW / OBS_PARTS worlds
+// only: at N = 4 it was the largest part of a wave's LDS (15.6 of 16.4 KB:
+// 10 waves per CU; with 2 parts 13.5 KB: 12, the VGPR bound).
+#ifndef BB_OBS_PARTS
+#define BB_OBS_PARTS 1
+#endif
 template <int N>
 struct SharedLds {
     static constexpr int WPW = WAVE / N;  // worlds per wave
+    // (N = 4 only: the lanes of a later part keep their sources in registers
+    // meanwhile -- at N = 10 that is 160 -> 256 VGPRs, no occupancy gained)
+    static constexpr int PARTS = N == 4 ? (BB_OBS_PARTS < WPW ? BB_OBS_PARTS : WPW) : 1;
+    static constexpr int SPP = (WPW + PARTS - 1) / PARTS;  // world slots per source-table part
     union {
         struct {
             World<N> world[WPW];
             uint32_t x[DppAgents<N>::value ? 1 : WAVE][XW];  // systems: per-agent exchange
         };
-        float e[WPW][ObsSrc<N>::ES];           // observation pass: row sources
+        float e[SPP][ObsSrc<N>::ES];           // observation pass: row sources of one part
     };
     uint4 code[BB_OBS_PIECES ? obs_width(N) / 4 : 1];  // PieceCode, 4 codes per piece
 };
@@ -1438,7 +1468,8 @@ struct LaneSources {
 // per observer a (the row loop is unrolled over a), before the loop: per
 // piece the loop does 4 LDS reads and one store; the row's team (obs 0-22
 // entries) is a wave-uniform offset.
-template <int N, int AUX>
+// Slots [S0, S1) of the wave's worlds, whose sources are at sm.e[slot - S0].
+template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
 __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
@@ -1457,8 +1488,9 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
         }
     }
     char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
-    for (int slot = 0; slot < WPW; slot++) {
-        const float *e = sm.e[slot];
+    static_assert(S1 <= WPW && S1 - S0 <= SharedLds<N>::SPP, "part of the source table");
+    for (int slot = S0; slot < S1; slot++) {
+        const float *e = sm.e[slot - S0];
 #pragma unroll
         for (int a = 0; a < N; a++) {
             const int r = slot * N + a;
@@ -1474,6 +1506,22 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
             }
         }
     }
+}
+
+// The source table written and emitted part by part (BB_OBS_PARTS): the
+// world state is dead once every lane holds its sources; each part's lanes
+// put theirs, the wave emits that part's rows, and the next part overlays it.
+template <int N, int AUX, int P = 0>
+__device__ __forceinline__ void obs_parts(SharedLds<N> &sm, const LaneSources<N> &src, uint64_t rows, float *obs,
+                                          int64_t row0, int lane, int slot, int k, bool active, bool share)
+{
+    using SL = SharedLds<N>;
+    constexpr int S0 = P * SL::SPP, S1 = (S0 + SL::SPP < SL::WPW) ? S0 + SL::SPP : SL::WPW;
+    __syncthreads();  // the world state (or the previous part) is dead: this part overlays it
+    if (active && slot >= S0 && slot < S1) src.put(sm.e[slot - S0], k, share);
+    __syncthreads();
+    emit_pieces<N, AUX, S0, S1>(sm, rows, obs, row0, lane);
+    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1>(sm, src, rows, obs, row0, lane, slot, k, active, share);
 }
 
 template <int N, int MODE, int PHASE = 0>
@@ -1593,12 +1641,9 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
             }
         }
         const uint64_t rows = __ballot(active && share);
-        __syncthreads();  // the world state is dead: the source table overlays it
-        if (active) src.put(sm.e[slot], k, share);
-        __syncthreads();
         // the row pass (memory-bound) ahead of other waves' systems (VALU)
         if constexpr (BB_PRIO_ROWS > 0) __builtin_amdgcn_s_setprio(BB_PRIO_ROWS);
-        emit_pieces<N, AUX>(sm, rows, p.c.obs, w0 * N, lane);
+        obs_parts<N, AUX>(sm, src, rows, p.c.obs, w0 * N, lane, slot, k, active, share);
         trace_point<MODE>(p, 9);
         return;
     }

@@ -84,8 +84,8 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
         policy_layers<MT>(x, R, norm, tile, c, q);
         pol_trace(a, first, 4, false);
         if constexpr (16 * MT < 64) {
-            __shared__ BucketLds<MT> bl;
-            bucket_pass_spread<MT>(a, tile, row0, lane, bl);
+            __shared__ BucketLds<16 * MT> bl;
+            bucket_pass_spread<16 * MT>(a, tile, row0, lane, bl);
             pol_wave_sync();
             pol_trace(a, first, 5, false);
             continue;

@@ -67,7 +67,7 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
     }
 }
 
-// Bucket pass of a tile of R = 16 MT < 64 rows: LPR = 64 / R lanes per row,
+// Bucket pass of R < 64 rows: LPR = 64 / R lanes per row,
 // every step the same instructions on different data (no divergent roles):
 //   A  lane part p: the Gumbel noise of logit pairs p, p + LPR, ... (one
 //      threefry call per pair) and, per logit, g = logit + noise and
@@ -77,19 +77,21 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
 //   C  lane part 0: the six terms summed in bucket order, the outputs.
 // Every value is the one pol_bucket_term / pol_select computes (same
 // operations on the same inputs), so rows are bit-identical to MT = 4's.
-// The bucket pass's LDS exchange of one wave (16 MT rows).
-template <int MT>
+// The bucket pass's LDS exchange of one wave (R rows).
+template <int R>
 struct BucketLds {
-    float g[16 * MT][POL_LOGITS + 1], e[16 * MT][POL_LOGITS + 1], t[16 * MT][POL_BUCKETS];
-    int32_t a[16 * MT][POL_BUCKETS];
+    float g[R][POL_LOGITS + 1], e[R][POL_LOGITS + 1], t[R][POL_BUCKETS];
+    int32_t a[R][POL_BUCKETS];
 };
 
-// act_local (optional): row r's six actions also into act_local[r] (LDS).
-template <int MT>
+// R rows (8, 16 or 32) over the wave's 64 lanes.  act_local (optional): row
+// r's six actions also into act_local[r] (LDS).
+template <int R>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
-                                                   BucketLds<MT> &buf, int32_t (*act_local)[6] = nullptr)
+                                                   BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr)
 {
-    constexpr int R = 16 * MT, LPR = 64 / R;
+    static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
+    constexpr int LPR = 64 / R;
     constexpr int PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
     float (*gbuf)[POL_LOGITS + 1] = buf.g, (*ebuf)[POL_LOGITS + 1] = buf.e, (*tbuf)[POL_BUCKETS] = buf.t;
     int32_t (*abuf)[POL_BUCKETS] = buf.a;
@@ -280,6 +282,99 @@ __device__ __forceinline__ void policy_layers(float (&x)[MT][32], const PolicyRe
         }
     }
     pol_wave_sync();
+}
+
+// LayerNorm + ReLU of rows 4q + i, i in [I0, I1), of a lane's accumulators
+// (the rows ln_relu_to_tile covers, the same operations).
+template <int I0, int I1>
+__device__ __forceinline__ void ln_relu_rows(f32x4 a0, f32x4 a1, float bias0, float bias1, float w0, float w1,
+                                             float lb0, float lb1, float (*tile)[33], int c, int q)
+{
+#pragma unroll
+    for (int i = I0; i < I1; i++) {
+        const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
+        const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
+        const float d0 = h0 - mean, d1 = h1 - mean;
+        const float var = quarter_sum((d0 * d0) + (d1 * d1)) * (1.0f / 32.0f);
+        const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
+        tile[4 * q + i][c] = pol_relu(((d0 * inv) * w0) + lb0);
+        tile[4 * q + i][c + 16] = pol_relu(((d1 * inv) * w1) + lb1);
+    }
+}
+
+// policy_layers<1> on one 16-row M-tile by two waves, h = 0 and 1: wave h
+// runs the accumulator chain of output columns 16h..16h+15 of every product
+// (the a0 / a1 chain of policy_layers, the same MFMA sequence) and the
+// LayerNorm of rows 4q + 2h, 4q + 2h + 1 (the same operations), the two halves
+// exchanged through `ex`.  bar(): a workgroup barrier both waves pass (5
+// calls).  Leaves row r's logits and value in ltile[r][0..19].
+struct HalfExchange {
+    f32x4 acc[2][64];  // [h][lane]
+};
+template <class Bar>
+__device__ __forceinline__ void policy_layers_half(float (&x)[32], const PolicyRegs &R, const float (*norm)[POL_IN],
+                                                   float (*tile)[33], float (*ltile)[33], HalfExchange &ex, int c,
+                                                   int q, int lane, int h, Bar bar)
+{
+    float nm[32], ni[32];
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        const float4 a4 = *(const float4 *)&norm[0][32 * q + 4 * v];
+        const float4 b4 = *(const float4 *)&norm[1][32 * q + 4 * v];
+        nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
+        ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 32; j++) x[j] = pol_clamp((x[j] - nm[j]) * ni[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[0][j], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[1][j], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    ex.acc[h][lane] = acc;
+    bar();
+    if (h == 0)
+        ln_relu_rows<0, 2>(ex.acc[0][lane], ex.acc[1][lane], R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1, tile, c, q);
+    else
+        ln_relu_rows<2, 4>(ex.acc[0][lane], ex.acc[1][lane], R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1, tile, c, q);
+    bar();
+    float hh[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) hh[j] = tile[c][8 * q + j];
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hh[j], R.w2[0][j], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hh[j], R.w2[1][j], acc, 0, 0, 0);
+    }
+    ex.acc[h][lane] = acc;
+    bar();
+    if (h == 0)
+        ln_relu_rows<0, 2>(ex.acc[0][lane], ex.acc[1][lane], R.b2_0, R.b2_1, R.l2w0, R.l2w1, R.l2b0, R.l2b1, tile, c, q);
+    else
+        ln_relu_rows<2, 4>(ex.acc[0][lane], ex.acc[1][lane], R.b2_0, R.b2_1, R.l2w0, R.l2w1, R.l2b0, R.l2b1, tile, c, q);
+    bar();
+#pragma unroll
+    for (int j = 0; j < 8; j++) hh[j] = tile[c][8 * q + j];
+    acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hh[j], R.wh[0][j], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(hh[j], R.wh[1][j], acc, 0, 0, 0);
+    }
+    const float bh = h == 0 ? R.bh0 : R.bh1;
+#pragma unroll
+    for (int i = 0; i < 4; i++) ltile[4 * q + i][c + 16 * h] = acc[i] + bh;
+    bar();
 }
 
 }  // namespace bb
