@@ -1005,6 +1005,17 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
 // 16h..16h+15 of every product and the LayerNorm of half the rows
 // (policy_layers_half: PPO_LAYER_BARS workgroup barriers per pass, which the
 // sim wave passes while it waits), then the bucket pass of 8 rows.
+// Workgroup barrier ordering LDS only: the waves of the PPO workgroup share
+// nothing through global memory inside the loop, so the barrier does not wait
+// for the wave's outstanding global stores (a __syncthreads() release fence
+// does: vmcnt(0) before every hand-off, ~1 us of write latency per step).
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 constexpr int PPO_PWAVES = 4;
 constexpr int PPO_LAYER_BARS = 5;
 constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
@@ -1075,7 +1086,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         }
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load pending into the loop
-    __syncthreads();  // setup: X holds the trainee rows of step 0, the erf table is in LDS
+    lds_barrier();  // setup: X holds the trainee rows of step 0, the erf table is in LDS
     for (int t = 0; t < r.steps; t++) {
         int lane_t = lane;
         int64_t w_t = w;
@@ -1085,8 +1096,8 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         Ctx c = make_ctx(p, w_t, k == 0);
         c.erf_tab = L.erf;
         const LaneAgents<N, MODE_FULL> ag{k, &p};
-        for (int b = 0; b < PPO_LAYER_BARS; b++) __syncthreads();  // (the policy pass's own barriers)
-        __syncthreads();  // the policy's actions are in LDS
+        for (int b = 0; b < PPO_LAYER_BARS; b++) lds_barrier();  // (the policy pass's own barriers)
+        lds_barrier();  // the policy's actions are in LDS
         ppo_trace(r, t, 0);
         int32_t ib = -1;
         bool share = false;
@@ -1139,7 +1150,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         }
         wave_sync();
         ppo_trace(r, t, 2);
-        __syncthreads();  // X holds the observations after step t
+        lds_barrier();  // X holds the observations after step t
     }
     if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
         int64_t w_s = w;
@@ -1148,7 +1159,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         store_world_agent(v, p, w_s * N + k, 0);
         if (k == 0) store_world_shared(v, p, w_s);
     }
-    for (int b = 0; b < PPO_LAYER_BARS; b++) __syncthreads();  // (the next-value pass's barriers)
+    for (int b = 0; b < PPO_LAYER_BARS; b++) lds_barrier();  // (the next-value pass's barriers)
 }
 
 __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
@@ -1176,12 +1187,16 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
         *(float4 *)&L.x[rr][4 * qq] = v4;
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    __syncthreads();  // setup
+    lds_barrier();  // setup
     PolicyArgs a{};
     a.rows = W;
     a.stochastic = r.stochastic;
     a.seed = r.seed;
-    auto bar = [] { __syncthreads(); };
+    auto bar = [] { lds_barrier(); };
+    // the Gumbel noise of a step depends on (seed, step, row, logit) only: each
+    // step's is drawn while the sim wave runs the step before it
+    BucketNoise<8> noise;
+    if (r.stochastic) bucket_noise<8>(noise, r.seed, r.step0, row0 + rh, W, lane);
     for (int t = 0; t <= r.steps; t++) {
         const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
         if (!final_pass && r.obs_out) {  // buffer.obs[t] = X, this wave's 8 rows
@@ -1203,11 +1218,14 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
-            bucket_pass_spread<8>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh);
+            bucket_pass_spread<8>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh,
+                                  r.stochastic ? &noise : nullptr);
             pol_wave_sync();
             if (pw == 0) ppo_trace(r, t, 3);
-            __syncthreads();  // actions in LDS
-            __syncthreads();  // X holds the observations after step t
+            lds_barrier();  // actions in LDS
+            if (r.stochastic && t + 1 < r.steps)
+                bucket_noise<8>(noise, r.seed, r.step0 + (uint32_t)(t + 1), row0 + rh, W, lane);
+            lds_barrier();  // X holds the observations after step t
         } else if (r.next_value && lane < 8 && row0 + rh + lane < W) {
             r.next_value[row0 + rh + lane] = L.ltile[m][rh + lane][POL_LOGITS];
         }

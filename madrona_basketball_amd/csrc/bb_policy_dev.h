@@ -84,11 +84,38 @@ struct BucketLds {
     int32_t a[R][POL_BUCKETS];
 };
 
+// The Gumbel noise a lane of the R-row bucket pass uses: logits 2 pr + h of
+// its pairs pr = part + LPR j (pol_gumbel's values).  It depends only on
+// (seed, step, row, logit), so a caller may compute it ahead of the logits.
+template <int R>
+struct BucketNoise {
+    static constexpr int LPR = 64 / R, PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR;
+    float g[PPL][2];
+};
+template <int R>
+__device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, uint32_t step, int64_t row0, int64_t rows,
+                                             int lane)
+{
+    using BN = BucketNoise<R>;
+    const int r = lane / BN::LPR, part = lane % BN::LPR;
+    const int64_t rr = row0 + r;
+#pragma unroll
+    for (int j = 0; j < BN::PPL; j++) {
+        const int pr = part + BN::LPR * j;
+        uint32_t b0 = 0, b1 = 0;
+        if (pr < BN::PAIRS && rr < rows) threefry2x32(seed, step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+#pragma unroll
+        for (int h = 0; h < 2; h++) n.g[j][h] = -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
+    }
+}
+
 // R rows (8, 16 or 32) over the wave's 64 lanes.  act_local (optional): row
-// r's six actions also into act_local[r] (LDS).
+// r's six actions also into act_local[r] (LDS).  pre (optional): this
+// lane's noise, computed ahead by bucket_noise with a's seed and step.
 template <int R>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
-                                                   BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr)
+                                                   BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr,
+                                                   const BucketNoise<R> *pre = nullptr)
 {
     static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
     constexpr int LPR = 64 / R;
@@ -114,7 +141,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         const int pr = part + LPR * j;
         if (pr < PAIRS) {
             uint32_t b0 = 0, b1 = 0;
-            if (stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+            if (stochastic && live && !pre) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int i = 2 * pr + h;
@@ -125,7 +152,8 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
                     for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
                     const float x = lg[i];
                     // pol_gumbel's value for logit i (its threefry word h)
-                    const float g = stochastic ? x + (-pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)))) : x;
+                    const float nz = pre ? pre->g[j][h] : -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
+                    const float g = stochastic ? x + nz : x;
                     gbuf[r][i] = g;
                     ebuf[r][i] = pol_expf(x - m);
                 }
