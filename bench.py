@@ -86,7 +86,7 @@ def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
     """The product's CPU executor in a child process (spawned before this
     process touches the GPU)."""
     import multiprocessing as mp
-    worlds = 16384
+    worlds = 2048 * max(1, threads)  # the oracle leg's total sample
     with mp.get_context("spawn").Pool(1) as pool:
         w, st, el = pool.apply(_executor_worker, ((num_agents, seconds, worlds, threads),))
     return {"value": w * st / el, "unit": "env-steps/s", "cores": threads, "kind": "product host executor",
