@@ -910,11 +910,13 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         r.steps = n; r.trainee = trainee; r.stochastic = stochastic ? 1 : 0; r.seed = seed; r.step0 = step0;
         uint64_t *ts = nullptr;
         const char *tr = std::getenv("MADRONA_BB_PPO_TRACE");  // diagnostics: per-step clocks of workgroup 0
-        if (tr && *tr && hipMalloc(&ts, (size_t)n * 4 * 8) == hipSuccess) r.diag_ts = ts;
+        const int64_t groups = (W + 31) / 32;
+        const size_t words = (size_t)n * 4 + 2 * (size_t)groups;  // per-step clocks of workgroup 0, per-workgroup span
+        if (tr && *tr && hipMalloc(&ts, words * 8) == hipSuccess) r.diag_ts = ts;
         hipError_t e = bb::launch_rollout_policy(s->n, s->p, r, st);
         if (e != hipSuccess) return hip_fail(e, "launch fused PPO rollout kernel");
         if (ts) {
-            std::vector<uint64_t> h((size_t)n * 4);
+            std::vector<uint64_t> h(words);
             if (hipMemcpyAsync(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
                 hipStreamSynchronize(st) == hipSuccess) {
                 FILE *f = std::fopen(tr, "a");
@@ -923,6 +925,9 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                         std::fprintf(f, "%d %llu %llu %llu %llu\n", k, (unsigned long long)h[4 * k],
                                      (unsigned long long)h[4 * k + 1], (unsigned long long)h[4 * k + 2],
                                      (unsigned long long)h[4 * k + 3]);
+                    for (int64_t b = 0; b < groups; b++)
+                        std::fprintf(f, "wg %lld %llu %llu\n", (long long)b, (unsigned long long)h[(size_t)n * 4 + 2 * b],
+                                     (unsigned long long)h[(size_t)n * 4 + 2 * b + 1]);
                     std::fclose(f);
                 }
             }

@@ -106,6 +106,16 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier ordering LDS only: a release fence at workgroup scope
+// over global memory too (__syncthreads) would wait for the wave's
+// outstanding global stores before every hand-off.
+__device__ __forceinline__ void lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <int N>
 struct ObsTile {
     static constexpr int QW = (obs_used(N) + 3) / 4;  // float4 pieces of a used row
@@ -637,11 +647,10 @@ struct Wide {
 constexpr uint32_t SHOT_PCT_UNSET = 0x7FC0BEEFu;  // a NaN the step never computes
 
 
-template <int N, int PHASE>
+template <int N, int PHASE, class T = typename Wide<N>::T>
 __device__ __forceinline__ void wide_obs_pass(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,
                                               int64_t w0, int64_t w, bool active, float *tile, float *obs)
 {
-    using T = typename Wide<N>::T;
     SharedObs<N> sh;
     lane_shared_obs(v, c, active, sh);
     const bool fast = active && canonical_slots(v, 0);
@@ -977,12 +986,161 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
     }
 }
 
-template <int N>
-__global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const RolloutArgs r)
+// MINW: waves per SIMD the register budget is sized for.  2 (256 registers)
+// spills the step loop's state (140 B of scratch per lane, reloaded on the
+// chain every step); 1 gives the wave the SIMD's whole file (VGPRs + AGPRs,
+// no scratch) and is taken while the grid is at most one wave per SIMD.
+template <int N, int MINW = 2>
+__global__ __launch_bounds__(WAVE, MINW) void k_rollout(const Params p, const RolloutArgs r)
 {
     if constexpr (FusedRollout<N>::value) {
         __shared__ float4 tile4[RolloutTile<N>::FLOATS / 4];
         rollout_agent_lanes<N>(p, r, (float *)tile4);
+    }
+}
+
+// K-step rollout over two waves per 32 worlds (C2-sized grids): the sim
+// wave S runs rollout_agent_lanes' step loop up to the reward / done records
+// and hands each lane's view of the world to the observation wave O through
+// LDS; O writes step t's observation rows while S runs the systems of step
+// t + 1.  Per step, with A / B the two workgroup barriers:
+//   S: systems(t), records(t)  A  view(t) -> LDS  B
+//   O:                         A                  B  LDS -> view(t), rows(t)
+// A: O has read view(t-1) (the buffer is free); B: view(t) is in LDS.  The
+// step's period is max(S's systems, O's rows) instead of their sum.  The rows
+// are emitted by the same pass code on the same view: bit-identical to
+// k_rollout.
+template <int N>
+struct SplitView {
+    static constexpr int WORDS = (int)(sizeof(World<N>) / 4) + 2;  // the view, inbounder id, obs_sharable
+    uint32_t w[WORDS][WAVE];  // word-major: word i of lane l at w[i][l]
+};
+
+template <int N>
+__device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArgs &r, SplitView<N> &view,
+                                               uint32_t *park_base)
+{
+    const int lane = (int)threadIdx.x;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const bool active = w < p.num_worlds;
+    const int64_t rows = p.num_worlds * N;
+    World<N> v;
+    uint32_t a_next[6 * N];
+    if (active) {
+        World<N> s;
+        load_world(s, p, w);
+        agent_view(s, v, lane % N);
+        load_words<6 * N>(r.actions, w, a_next);
+    }
+    const double *erf_tab = erf_table_lds();
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    for (int t = 0; t < r.steps; t++) {
+        int lane_t = lane;
+        int64_t w_t = w;
+        __asm__ volatile("" : "+v"(lane_t));
+        __asm__ volatile("" : "+v"(w_t));
+        const int k = lane_t % N;
+        const int64_t row = w_t * N + k;
+        Ctx c = make_ctx(p, w_t, k == 0);
+        c.erf_tab = erf_tab;
+        const LaneAgents<N, MODE_FULL> ag{k, &p};
+        int32_t *act_t = r.actions + (int64_t)t * rows * 6;
+        uint32_t *park = park_base + lane_t;
+        int32_t ib = -1;
+        bool share = false;
+        if (active) {
+            World<N> s;
+            agent_view<N, true>(v, s, k);
+#pragma unroll
+            for (int i = 0; i < N; i++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) s.act[i][q] = (int32_t)a_next[6 * i + q];
+#pragma unroll
+            for (int q = 0; q < 6; q++) park[q * WAVE] = (uint32_t)pick_by<N>(k, [&](int j) { return s.act[j][q]; });
+            load_words<6 * N>(t + 1 < r.steps ? act_t + rows * 6 : act_t, w_t, a_next);
+            step_world_pre_obs(s, c, ag);
+#pragma unroll
+            for (int q = 0; q < 6 * N; q++) __asm__ volatile("" : "+v"(a_next[q]));
+            ib = inbounder_id(s);
+            share = obs_sharable(s);
+            agent_view(s, v, k);
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
+            r.done[(int64_t)t * r.rd_step + row] = v.done[0];
+            bool changed = false;
+#pragma unroll
+            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
+            if (changed) {
+                uint32_t a[6];
+#pragma unroll
+                for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
+                store_words<6>(act_t, row, a);
+            }
+        }
+        lds_barrier();  // A: the observation wave has read view(t-1)
+        {
+            uint32_t u[SplitView<N>::WORDS];
+            __builtin_memcpy(u, &v, sizeof(World<N>));
+            u[SplitView<N>::WORDS - 2] = (uint32_t)ib;
+            u[SplitView<N>::WORDS - 1] = share ? 1u : 0u;
+#pragma unroll
+            for (int i = 0; i < SplitView<N>::WORDS; i++) view.w[i][lane_t] = u[i];
+        }
+        lds_barrier();  // B: view(t) is in LDS
+    }
+    if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
+        int64_t w_s = w;
+        __asm__ volatile("" : "+v"(w_s));
+        const int k = lane % N;
+        store_world_agent(v, p, w_s * N + k, 0);
+        if (k == 0) store_world_shared(v, p, w_s);
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArgs &r, const SplitView<N> &view,
+                                               float *tile)
+{
+    using T = RolloutTile<N>;
+    const int lane = (int)threadIdx.x % WAVE;
+    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    for (int t = 0; t < r.steps; t++) {
+        int lane_t = lane;
+        __asm__ volatile("" : "+v"(lane_t));
+        const int64_t w = w0 + lane_t / N;
+        const bool active = w < p.num_worlds;
+        const int k = lane_t % N;
+        lds_barrier();  // A
+        lds_barrier();  // B
+        World<N> v;
+        uint32_t u[SplitView<N>::WORDS];
+#pragma unroll
+        for (int i = 0; i < SplitView<N>::WORDS; i++) u[i] = view.w[i][lane_t];
+        __builtin_memcpy(&v, u, sizeof(World<N>));
+        const int32_t ib = (int32_t)u[SplitView<N>::WORDS - 2];
+        const bool share = u[SplitView<N>::WORDS - 1] != 0u;
+        const Ctx c = make_ctx(p, w, k == 0);
+        float *obs = r.obs + (int64_t)t * r.obs_step;
+        wide_obs_pass<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+        wave_sync();  // the tile is rewritten by the next pass
+        if constexpr (T::PH > 1) {
+            wide_obs_pass<N, 1, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+            wave_sync();
+        }
+        static_assert(T::PH <= 2, "two row passes");
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, const RolloutArgs r)
+{
+    if constexpr (FusedRollout<N>::value) {
+        __shared__ SplitView<N> view;
+        __shared__ float4 tile4[RolloutTile<N>::FLOATS / 4];
+        __shared__ uint32_t park[6 * WAVE];
+        if (__builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE) == 0) split_sim_wave<N>(p, r, view, park);
+        else split_obs_wave<N>(p, r, view, (float *)tile4);
     }
 }
 
@@ -1005,17 +1163,10 @@ __global__ __launch_bounds__(WAVE, 2) void k_rollout(const Params p, const Rollo
 // 16h..16h+15 of every product and the LayerNorm of half the rows
 // (policy_layers_half: PPO_LAYER_BARS workgroup barriers per pass, which the
 // sim wave passes while it waits), then the bucket pass of 8 rows.
-// Workgroup barrier ordering LDS only: the waves of the PPO workgroup share
-// nothing through global memory inside the loop, so the barrier does not wait
-// for the wave's outstanding global stores (a __syncthreads() release fence
-// does: vmcnt(0) before every hand-off, ~1 us of write latency per step).
-__device__ __forceinline__ void lds_barrier()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
-
+// The waves of the PPO workgroup share nothing through global memory inside
+// the loop, so their hand-offs are lds_barrier()s, which do not wait for the
+// wave's outstanding global stores (a __syncthreads() release fence does:
+// vmcnt(0) before every hand-off, ~1 us of write latency per step).
 constexpr int PPO_PWAVES = 4;
 constexpr int PPO_LAYER_BARS = 5;
 constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
@@ -1061,10 +1212,20 @@ __device__ __forceinline__ void ppo_trace(const PolicyRolloutArgs &r, int t, int
     }
 }
 
+// diagnostics: every workgroup's sim-wave start (0) and end (1) clocks at
+// diag_ts[steps * 4 + 2 * workgroup + which]
+__device__ __forceinline__ void ppo_trace_wg(const PolicyRolloutArgs &r, int which)
+{
+    if (r.diag_ts) {
+        const uint64_t c = wall_clock64();
+        if (threadIdx.x == 0) r.diag_ts[(int64_t)r.steps * 4 + 2 * blockIdx.x + which] = c;
+    }
+}
+
 template <int N>
 __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, float *tile)
 {
-    using T = StepTile<N, false>;
+    ppo_trace_wg(r, 0);
     const int lane = threadIdx.x;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
     const int64_t w = w0 + lane / N;
@@ -1160,6 +1321,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         if (k == 0) store_world_shared(v, p, w_s);
     }
     for (int b = 0; b < PPO_LAYER_BARS; b++) lds_barrier();  // (the next-value pass's barriers)
+    ppo_trace_wg(r, 1);
 }
 
 __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
@@ -1873,6 +2035,18 @@ bool step_wide(int64_t num_worlds)
     }
 }
 
+// Compute units of the current device (256 on MI355X).
+static unsigned device_cus()
+{
+    static const unsigned v = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        return (unsigned)cus;
+    }();
+    return v;
+}
+
 template <int N>
 hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
@@ -1906,6 +2080,29 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
     return hipGetLastError();
 }
 
+// The whole-register-file rollout while the grid fits one wave per SIMD (every
+// CU of the device, 4 SIMDs each); env MADRONA_BB_ROLLOUT_MINW=1/2 forces it.
+static bool rollout_minw1(unsigned waves)
+{
+    const char *e = getenv("MADRONA_BB_ROLLOUT_MINW");
+    const int forced = e && *e ? atoi(e) : 0;
+    if (forced) return forced == 1;
+    return waves <= 4u * device_cus();
+}
+
+// k_rollout_split while its workgroups (2 waves) fit one wave per SIMD:
+// at most 2 per CU.  MADRONA_BB_ROLLOUT_SPLIT=0/1 forces it off / on (A/B).
+#ifndef BB_ROLLOUT_SPLIT
+#define BB_ROLLOUT_SPLIT 1
+#endif
+static bool rollout_split(unsigned groups)
+{
+    const char *e = getenv("MADRONA_BB_ROLLOUT_SPLIT");  // read per launch: the tests run both kernels
+    const int forced = e && *e ? atoi(e) : -1;
+    const bool on = forced >= 0 ? forced != 0 : BB_ROLLOUT_SPLIT != 0;
+    return on && groups <= 2u * device_cus();
+}
+
 template <int N>
 hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
@@ -1914,7 +2111,12 @@ hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s
     } else {
         constexpr int WPB = Lanes<N>::WPB;
         const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-        hipExtLaunchKernelGGL(k_rollout<N>, grid, block, 0, s, ev0, ev1, 0, p, r);
+        if (rollout_split(grid.x))
+            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
+        else if (rollout_minw1(grid.x))
+            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        else
+            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2>), grid, block, 0, s, ev0, ev1, 0, p, r);
         return hipGetLastError();
     }
 }

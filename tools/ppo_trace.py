@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, default=8192)
     ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     path = os.path.join(tempfile.mkdtemp(), "ppo_trace.txt")
     os.environ["MADRONA_BB_PPO_TRACE"] = path
@@ -27,10 +28,17 @@ def main():
                                        per_world_rng=True)
     pol = FusedPolicy.from_agent(make_agent(0).cuda())
     b = pol.rollout_buffers(sim, a.steps)
-    for i in range(3):
-        pol.rollout(sim, a.steps, b, seed=1, step0=i * a.steps)
+    ev = []
+    for i in range(a.reps):
+        ev.append(pol.rollout(sim, a.steps, b, seed=1, step0=i * a.steps, time_kernels=True) * 1e3)
     torch.cuda.synchronize()
-    rows = np.loadtxt(path, dtype=np.int64)[-a.steps:]
+    print(f"event us per rollout (first, median, last of {a.reps}): {ev[0]:.1f} {sorted(ev)[len(ev) // 2]:.1f} {ev[-1]:.1f}")
+    lines = open(path).read().split("\n")
+    steps = [l for l in lines if l and not l.startswith("wg")]
+    wgs = [l for l in lines if l.startswith("wg")]
+    G = (a.worlds + 31) // 32
+    rows = np.array([[int(x) for x in l.split()] for l in steps[-a.steps:]], dtype=np.int64)
+    wg = np.array([[int(x) for x in l.split()[1:]] for l in wgs[-G:]], dtype=np.int64)
     t = rows[:, 1:5]
     d_sys = (t[:, 1] - t[:, 0]) * 10
     d_obs = (t[:, 2] - t[:, 1]) * 10
@@ -39,6 +47,15 @@ def main():
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 50, 100)]
     print(f"worlds {a.worlds}: ns per step {pct(step)}; S systems+reward {pct(d_sys)}; S rows {pct(d_obs)}; "
           f"P policy {pct(d_pol)}; barrier hand-offs {pct(step[:] - d_sys[1:] - d_obs[1:] - d_pol)}")
+    t0 = wg[:, 1].min()
+    span = (wg[:, 2] - wg[:, 1]) * 10
+    start = (wg[:, 1] - t0) * 10
+    end = (wg[:, 2] - t0) * 10
+    pq = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
+    w0 = wg[wg[:, 0] == 0][0]
+    print(f"  workgroups {G}: start ns {pq(start)}; span ns {pq(span)}; end ns {pq(end)}; "
+          f"wg0 setup {(t[0, 0] - w0[1]) * 10} ns, steps {(t[-1, 2] - t[0, 0]) * 10} ns, "
+          f"tail {(w0[2] - t[-1, 2]) * 10} ns")
 
 
 if __name__ == "__main__":
