@@ -17,6 +17,8 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <pthread.h>
+#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -150,7 +152,20 @@ class HostPool {
 public:
     explicit HostPool(int n) : n_(n < 1 ? 1 : n)
     {
-        for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { worker(t); });
+        // Every share on a pool thread pinned to its own CPU of the process's
+        // affinity set, the caller only waiting (BB_CPU_PIN=0: the caller is
+        // worker 0 and nothing is pinned).  Measured on 8 host cores, 2 048
+        // worlds per thread: 2 threads 3.36 -> 3.97 M env-steps/s (1 thread:
+        // 2.2), 8 threads 11.5 -> 11.8.
+        const char *pin = std::getenv("BB_CPU_PIN");
+        pinned_ = !(pin && *pin == '0') && n_ > 1;
+        cpu_set_t allowed;
+        CPU_ZERO(&allowed);
+        if (pinned_ && sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
+            for (int c = 0; c < CPU_SETSIZE; c++)
+                if (CPU_ISSET(c, &allowed)) cpus_.push_back(c);
+        }
+        for (int t = pinned_ ? 0 : 1; t < n_; t++) th_.emplace_back([this, t] { worker(t); });
     }
     ~HostPool()
     {
@@ -169,11 +184,11 @@ public:
         {
             std::lock_guard<std::mutex> g(m_);
             job_ = &f;
-            left_.store(n_ - 1, std::memory_order_relaxed);
+            left_.store(pinned_ ? n_ : n_ - 1, std::memory_order_relaxed);
             gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
-        f(0);
+        if (!pinned_) f(0);
         // the others: spin, then sleep
         for (int i = 0; left_.load(std::memory_order_acquire) != 0; i++) {
             if (i > 4096) {
@@ -189,6 +204,12 @@ public:
 private:
     void worker(int t)
     {
+        if (pinned_ && !cpus_.empty()) {
+            cpu_set_t one;
+            CPU_ZERO(&one);
+            CPU_SET(cpus_[(size_t)t % cpus_.size()], &one);
+            (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
+        }
         uint64_t seen = 0;
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
@@ -216,6 +237,8 @@ private:
         }
     }
     const int n_;
+    bool pinned_ = false;
+    std::vector<int> cpus_;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_cv_;
