@@ -64,9 +64,16 @@ constexpr int32_t HOOP0_ID = 0, HOOP1_ID = 1, BALL_ID = 2, AGENT0_ID = 3;
 constexpr uint32_t FLAG_PER_WORLD_RNG = 0x1u, FLAG_NO_TAG_MASK = 0x2u, FLAG_FULL_GAME = 0x4u;
 
 BB_HD constexpr int obs_used(int n) { return 61 + 38 * (n - 1) + 2 * n; }
+// BB_OBS_ROW_ALIGN (floats, diagnostic builds): rows wider than 128 floats
+// (N > 2) end on this boundary; the product keeps 4 (16-byte pieces).
+#ifndef BB_OBS_ROW_ALIGN
+#define BB_OBS_ROW_ALIGN 4
+#endif
 BB_HD constexpr int obs_width(int n)
 {
-    return ((obs_used(n) + 3) & ~3) < 128 ? 128 : ((obs_used(n) + 3) & ~3);
+    return ((obs_used(n) + 3) & ~3) < 128
+               ? 128
+               : ((obs_used(n) + BB_OBS_ROW_ALIGN - 1) / BB_OBS_ROW_ALIGN * BB_OBS_ROW_ALIGN);
 }
 
 // ------------------------------------------------------------------ vec math
