@@ -934,7 +934,8 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         uint64_t *ts = nullptr;
         const char *tr = std::getenv("MADRONA_BB_PPO_TRACE");  // diagnostics: per-step clocks of workgroup 0
         const int64_t groups = (W + 31) / 32;
-        const size_t words = (size_t)n * 4 + 2 * (size_t)groups;  // per-step clocks of workgroup 0, per-workgroup span
+        const size_t TP = 16;  // PPO_TRACE_POINTS (bb_kernels.hip)
+        const size_t words = (size_t)n * TP + 2 * (size_t)groups;  // per-step clocks of workgroup 0, per-workgroup span
         if (tr && *tr && hipMalloc(&ts, words * 8) == hipSuccess) r.diag_ts = ts;
         hipError_t e = bb::launch_rollout_policy(s->n, s->p, r, st);
         if (e != hipSuccess) return hip_fail(e, "launch fused PPO rollout kernel");
@@ -944,13 +945,14 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 hipStreamSynchronize(st) == hipSuccess) {
                 FILE *f = std::fopen(tr, "a");
                 if (f) {
-                    for (int32_t k = 0; k < n; k++)
-                        std::fprintf(f, "%d %llu %llu %llu %llu\n", k, (unsigned long long)h[4 * k],
-                                     (unsigned long long)h[4 * k + 1], (unsigned long long)h[4 * k + 2],
-                                     (unsigned long long)h[4 * k + 3]);
+                    for (int32_t k = 0; k < n; k++) {
+                        std::fprintf(f, "%d", k);
+                        for (size_t i = 0; i < TP; i++) std::fprintf(f, " %llu", (unsigned long long)h[TP * k + i]);
+                        std::fprintf(f, "\n");
+                    }
                     for (int64_t b = 0; b < groups; b++)
-                        std::fprintf(f, "wg %lld %llu %llu\n", (long long)b, (unsigned long long)h[(size_t)n * 4 + 2 * b],
-                                     (unsigned long long)h[(size_t)n * 4 + 2 * b + 1]);
+                        std::fprintf(f, "wg %lld %llu %llu\n", (long long)b, (unsigned long long)h[(size_t)n * TP + 2 * b],
+                                     (unsigned long long)h[(size_t)n * TP + 2 * b + 1]);
                     std::fclose(f);
                 }
             }

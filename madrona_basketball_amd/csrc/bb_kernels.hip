@@ -1203,22 +1203,26 @@ struct LdsRowSink {
 
 // diagnostics (PolicyRolloutArgs::diag_ts, workgroup 0): per step k the clock
 // at 0 S starts the step, 1 S's systems + reward done, 2 S's observation rows
-// done, 3 the first policy wave's actions done (for step k)
+// done, 3 the first policy wave's actions done (for step k); the first policy
+// wave's pass for step k: 4 start (X holds the rows), 5 obs_out recorded, 6 X
+// in registers, 7-11 at the five barriers of the layers (after each), 12
+// bucket pass done.
+constexpr int PPO_TRACE_POINTS = 16;
 __device__ __forceinline__ void ppo_trace(const PolicyRolloutArgs &r, int t, int point)
 {
     if (r.diag_ts && blockIdx.x == 0) {
         const uint64_t c = wall_clock64();
-        if (threadIdx.x % WAVE == 0) r.diag_ts[(int64_t)t * 4 + point] = c;
+        if (threadIdx.x % WAVE == 0) r.diag_ts[(int64_t)t * PPO_TRACE_POINTS + point] = c;
     }
 }
 
 // diagnostics: every workgroup's sim-wave start (0) and end (1) clocks at
-// diag_ts[steps * 4 + 2 * workgroup + which]
+// diag_ts[steps * PPO_TRACE_POINTS + 2 * workgroup + which]
 __device__ __forceinline__ void ppo_trace_wg(const PolicyRolloutArgs &r, int which)
 {
     if (r.diag_ts) {
         const uint64_t c = wall_clock64();
-        if (threadIdx.x == 0) r.diag_ts[(int64_t)r.steps * 4 + 2 * blockIdx.x + which] = c;
+        if (threadIdx.x == 0) r.diag_ts[(int64_t)r.steps * PPO_TRACE_POINTS + 2 * blockIdx.x + which] = c;
     }
 }
 
@@ -1276,15 +1280,9 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             ib = inbounder_id(s);
             share = obs_sharable(s);
             agent_view(s, v, k);
-            sys_reward_agent(v, 0, AGENT0_ID + k);
-            ppo_trace(r, t, 1);
-            if (k == trainee) {
-                if (r.reward) {
-                    r.reward[(int64_t)t * p.num_worlds + w_t] = v.rew[0];
-                    r.done[(int64_t)t * p.num_worlds + w_t] = v.done[0];
-                }
-            }
         }
+        ppo_trace(r, t, 1);
+        lds_barrier();  // X is free: the policy waves have recorded buffer.obs[t] from it
         // the trainee's next observation row into X
         {
             SharedObs<N> sh;
@@ -1312,6 +1310,15 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         wave_sync();
         ppo_trace(r, t, 2);
         lds_barrier();  // X holds the observations after step t
+        // reward (read by nothing on the way to the next actions) while the
+        // policy waves run the network on X
+        if (active) {
+            sys_reward_agent(v, 0, AGENT0_ID + k);
+            if (k == trainee && r.reward) {
+                r.reward[(int64_t)t * p.num_worlds + w_t] = v.rew[0];
+                r.done[(int64_t)t * p.num_worlds + w_t] = v.done[0];
+            }
+        }
     }
     if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
         int64_t w_s = w;
@@ -1361,32 +1368,48 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     if (r.stochastic) bucket_noise<8>(noise, r.seed, r.step0, row0 + rh, W, lane);
     for (int t = 0; t <= r.steps; t++) {
         const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
-        if (!final_pass && r.obs_out) {  // buffer.obs[t] = X, this wave's 8 rows
-            for (int i = lane; i < 8 * 32; i += WAVE) {
-                const int rr = r0 + rh + i / 32, qq = i % 32;
-                const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
-                if (wg < W) *(float4 *)(r.obs_out + ((int64_t)t * W + wg) * POL_IN + 4 * qq) = *(const float4 *)&L.x[rr][4 * qq];
-            }
-        }
+        const bool tr = pw == 0 && !final_pass;
+        if (tr) ppo_trace(r, t, 4);
+        if (tr) ppo_trace(r, t, 5);
         float x[32];
 #pragma unroll
         for (int v = 0; v < 8; v++) {
             const float4 o = *(const float4 *)&L.x[r0 + c][32 * q + 4 * v];
             x[4 * v] = o.x; x[4 * v + 1] = o.y; x[4 * v + 2] = o.z; x[4 * v + 3] = o.w;
         }
-        policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, bar);
+        if (r.diag_ts) {  // (diagnostics: the loads retired here, and a clock at every barrier)
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            if (tr) ppo_trace(r, t, 6);
+            int nb = 0;
+            auto tbar = [&] { if (tr) ppo_trace(r, t, 7 + nb); nb++; lds_barrier(); };
+            policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, tbar);
+        } else {
+            policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, bar);
+        }
         a.step = r.step0 + (uint32_t)t;
         if (!final_pass) {
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
             bucket_pass_spread<8>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh,
-                                  r.stochastic ? &noise : nullptr);
+                                  r.stochastic ? &noise : nullptr,
+                                  (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 12 : nullptr);
             pol_wave_sync();
             if (pw == 0) ppo_trace(r, t, 3);
             lds_barrier();  // actions in LDS
+            // while the sim wave steps: buffer.obs[t] = X (this wave's 8 rows),
+            // then the next step's Gumbel noise
+            if (r.obs_out) {
+                for (int i = lane; i < 8 * 32; i += WAVE) {
+                    const int rr = r0 + rh + i / 32, qq = i % 32;
+                    const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
+                    if (wg < W)
+                        *(float4 *)(r.obs_out + ((int64_t)t * W + wg) * POL_IN + 4 * qq) = *(const float4 *)&L.x[rr][4 * qq];
+                }
+            }
             if (r.stochastic && t + 1 < r.steps)
                 bucket_noise<8>(noise, r.seed, r.step0 + (uint32_t)(t + 1), row0 + rh, W, lane);
+            lds_barrier();  // X is free (the sim wave rewrites it next)
             lds_barrier();  // X holds the observations after step t
         } else if (r.next_value && lane < 8 && row0 + rh + lane < W) {
             r.next_value[row0 + rh + lane] = L.ltile[m][rh + lane][POL_LOGITS];

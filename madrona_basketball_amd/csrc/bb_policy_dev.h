@@ -112,10 +112,19 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
 // R rows (8, 16 or 32) over the wave's 64 lanes.  act_local (optional): row
 // r's six actions also into act_local[r] (LDS).  pre (optional): this
 // lane's noise, computed ahead by bucket_noise with a's seed and step.
+// ts (diagnostics, optional): lane 0 writes the clock after the maxima, the
+// per-logit part, the per-bucket part and the outputs into ts[0..3].
+__device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
+{
+    if (ts) {
+        const uint64_t c = wall_clock64();
+        if (lane == 0) ts[i] = c;
+    }
+}
 template <int R>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
                                                    BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr,
-                                                   const BucketNoise<R> *pre = nullptr)
+                                                   const BucketNoise<R> *pre = nullptr, uint64_t *ts = nullptr)
 {
     static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
     constexpr int LPR = 64 / R;
@@ -136,6 +145,8 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         for (int i = 1; i < nb; i++) m = lg[o + i] > m ? lg[o + i] : m;
         mx[b] = m;
     }
+    if (ts) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (diagnostics)
+    bucket_stamp(ts, 0, lane);
 #pragma unroll
     for (int j = 0; j < PPL; j++) {
         const int pr = part + LPR * j;
@@ -161,6 +172,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         }
     }
     pol_wave_sync();
+    bucket_stamp(ts, 1, lane);
 #pragma unroll
     for (int j = 0; j < BPL; j++) {
         const int b = part + LPR * j;
@@ -185,6 +197,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         }
     }
     pol_wave_sync();
+    bucket_stamp(ts, 2, lane);
     if (part == 0 && live) {
         float term[POL_BUCKETS];
         int32_t act[POL_BUCKETS];
@@ -212,6 +225,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
             a.done_out[rr] = a.done_src[rr * a.rd_stride];
         }
     }
+    bucket_stamp(ts, 3, lane);
 }
 
 // The B operands and the per-column constants of one lane, loaded once per

@@ -38,6 +38,14 @@ def main():
     wgs = [l for l in lines if l.startswith("wg")]
     G = (a.worlds + 31) // 32
     rows = np.array([[int(x) for x in l.split()] for l in steps[-a.steps:]], dtype=np.int64)
+    # the first policy wave's pass for step k (points 4..12): obs_out record,
+    # X into registers, layer 1 + its barrier, LayerNorm 1, layer 2, LayerNorm
+    # 2, heads, bucket pass
+    P = rows[:, 5:17]
+    names = ["(start)", "X -> registers", "layer 1 MFMA", "LN 1 (+bar)", "layer 2 MFMA (+bar)",
+             "LN 2 (+bar)", "heads (+bar)", "bucket maxima", "bucket per-logit", "bucket per-bucket",
+             "bucket outputs"]
+    sub = {n: [int(np.percentile((P[:, i + 1] - P[:, i]) * 10, q)) for q in (0, 50, 100)] for i, n in enumerate(names)}
     wg = np.array([[int(x) for x in l.split()[1:]] for l in wgs[-G:]], dtype=np.int64)
     t = rows[:, 1:5]
     d_sys = (t[:, 1] - t[:, 0]) * 10
@@ -45,8 +53,11 @@ def main():
     d_pol = (t[1:, 3] - t[:-1, 2]) * 10  # policy for step k+1 after the rows of step k
     step = (t[1:, 0] - t[:-1, 0]) * 10
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 50, 100)]
-    print(f"worlds {a.worlds}: ns per step {pct(step)}; S systems+reward {pct(d_sys)}; S rows {pct(d_obs)}; "
+    print(f"worlds {a.worlds}: ns per step {pct(step)}; S systems {pct(d_sys)}; S X free + rows {pct(d_obs)}; "
           f"P policy {pct(d_pol)}; barrier hand-offs {pct(step[:] - d_sys[1:] - d_obs[1:] - d_pol)}")
+    wait = (P[1:, 0] - t[:-1, 2]) * 10  # S's rows done -> P's pass starts
+    print(f"  P pass ns (min, median, max): rows ready -> P start {pct(wait)}; "
+          + "; ".join(f"{n} {v}" for n, v in sub.items()))
     t0 = wg[:, 1].min()
     span = (wg[:, 2] - wg[:, 1]) * 10
     start = (wg[:, 1] - t0) * 10
