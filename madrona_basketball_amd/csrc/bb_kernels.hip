@@ -1276,7 +1276,9 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             for (int i = 0; i < N; i++)
 #pragma unroll
                 for (int q = 0; q < 6; q++) s.act[i][q] = i == trainee ? a[q] : s.act[i][q];
+#if !defined(BB_PPO_NO_SYS)  // (diagnostic timing builds only: no systems)
             step_world_pre_obs(s, c, ag);
+#endif
             ib = inbounder_id(s);
             share = obs_sharable(s);
             agent_view(s, v, k);
@@ -1391,9 +1393,11 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
-            bucket_pass_spread<8>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh,
-                                  r.stochastic ? &noise : nullptr,
-                                  (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 12 : nullptr);
+            uint64_t *bts = (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 12 : nullptr;
+            if (r.stochastic)
+                bucket_pass_spread<8, true>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise, bts);
+            else
+                bucket_pass_spread<8, false>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr, bts);
             pol_wave_sync();
             if (pw == 0) ppo_trace(r, t, 3);
             lds_barrier();  // actions in LDS

@@ -121,7 +121,9 @@ __device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
         if (lane == 0) ts[i] = c;
     }
 }
-template <int R>
+// PRE (compile-time, so that the noise stays in registers: a runtime-null
+// pointer to it would put it in scratch): `pre` holds this lane's noise.
+template <int R, bool PRE = false>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
                                                    BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr,
                                                    const BucketNoise<R> *pre = nullptr, uint64_t *ts = nullptr)
@@ -152,7 +154,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         const int pr = part + LPR * j;
         if (pr < PAIRS) {
             uint32_t b0 = 0, b1 = 0;
-            if (stochastic && live && !pre) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+            if (!PRE && stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 const int i = 2 * pr + h;
@@ -163,7 +165,9 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
                     for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
                     const float x = lg[i];
                     // pol_gumbel's value for logit i (its threefry word h)
-                    const float nz = pre ? pre->g[j][h] : -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
+                    float nz;
+                    if constexpr (PRE) nz = pre->g[j][h];
+                    else nz = -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
                     const float g = stochastic ? x + nz : x;
                     gbuf[r][i] = g;
                     ebuf[r][i] = pol_expf(x - m);
