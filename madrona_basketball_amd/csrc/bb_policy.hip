@@ -54,11 +54,10 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
     pol_trace(a, true, 1, true);
 
     const int64_t tiles = (a.rows + 16 * MT - 1) / (16 * MT);
-    for (int64_t tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
-        const int64_t row0 = tl * 16 * MT;
-        const bool first = tl == blockIdx.x;
-        // every M-tile's 32 observation floats per lane, loads issued together
-        float x[MT][32];
+    // every M-tile's 32 observation floats per lane, loads issued together;
+    // in a grid-stride loop the next tile's rows are loaded while this tile
+    // is computed
+    auto load_rows = [&](int64_t row0, float (&x)[MT][32]) {
 #pragma unroll
         for (int m = 0; m < MT; m++) {
             const int64_t r = row0 + 16 * m + c;
@@ -69,15 +68,41 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
                     const float4 o = src[v];
                     x[m][4 * v] = o.x; x[m][4 * v + 1] = o.y; x[m][4 * v + 2] = o.z; x[m][4 * v + 3] = o.w;
                 }
-                if (a.obs_out) {  // the rollout's record of the observed row (buffer.obs, ppo.py:129)
+            } else {
+#pragma unroll
+                for (int j = 0; j < 32; j++) x[m][j] = 0.f;
+            }
+        }
+    };
+    // (PREFETCH: 64-row tiles, whose kernel holds a wave per SIMD anyway; at
+    // MT = 1 the second row set would cost the two waves per SIMD)
+    constexpr bool PREFETCH = MT == 4;
+    float xn[PREFETCH ? MT : 1][32];
+    if constexpr (PREFETCH)
+        if ((int64_t)blockIdx.x < tiles) load_rows((int64_t)blockIdx.x * 16 * MT, xn);
+    for (int64_t tl = blockIdx.x; tl < tiles; tl += gridDim.x) {
+        const int64_t row0 = tl * 16 * MT;
+        const bool first = tl == blockIdx.x;
+        float x[MT][32];
+        if constexpr (PREFETCH) {
+#pragma unroll
+            for (int m = 0; m < MT; m++)
+#pragma unroll
+                for (int j = 0; j < 32; j++) x[m][j] = xn[m][j];
+            if (tl + gridDim.x < tiles) load_rows((tl + gridDim.x) * 16 * MT, xn);
+        } else {
+            load_rows(row0, x);
+        }
+        if (a.obs_out) {  // the rollout's record of the observed rows (buffer.obs, ppo.py:129)
+#pragma unroll
+            for (int m = 0; m < MT; m++) {
+                const int64_t r = row0 + 16 * m + c;
+                if (r < a.rows) {
                     float4 *dst = (float4 *)(a.obs_out + r * POL_IN + 32 * q);
 #pragma unroll
                     for (int v = 0; v < 8; v++)
                         dst[v] = make_float4(x[m][4 * v], x[m][4 * v + 1], x[m][4 * v + 2], x[m][4 * v + 3]);
                 }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 32; j++) x[m][j] = 0.f;
             }
         }
         pol_trace(a, first, 2, true);
@@ -147,7 +172,17 @@ static hipError_t launch_policy_mt(const PolicyArgs &a, hipStream_t s)
 {
     const int64_t tiles = (a.rows + 16 * MT - 1) / (16 * MT);
     if (tiles <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)(tiles < 16384 ? tiles : 16384);  // grid-stride beyond
+    // grid-stride beyond this many waves: 64-row tiles one wave per SIMD
+    // (1 024 on the 256 CUs), the next tile's rows loaded under this one's
+    // network (131 072 rows: 46.8 -> 43.5 us argmax, 57.1 -> 54.4 sampled;
+    // profiles/r03/ah_policy_grid_ab.txt); MADRONA_BB_POLICY_GRID overrides
+    static const int64_t forced = [] {
+        const char *e = getenv("MADRONA_BB_POLICY_GRID");
+        const long g = e && *e ? atol(e) : 0;
+        return (int64_t)(g > 0 ? g : 0);
+    }();
+    const int64_t cap = forced ? forced : (MT == 4 ? 1024 : 16384);
+    const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
     hipLaunchKernelGGL(k_policy<MT>, dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
 }
