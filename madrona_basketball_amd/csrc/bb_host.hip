@@ -152,13 +152,14 @@ class HostPool {
 public:
     explicit HostPool(int n) : n_(n < 1 ? 1 : n)
     {
-        // Every share on a pool thread pinned to its own CPU of the process's
-        // affinity set, the caller only waiting (BB_CPU_PIN=0: the caller is
-        // worker 0 and nothing is pinned).  Measured on 8 host cores, 2 048
-        // worlds per thread: 2 threads 3.36 -> 3.97 M env-steps/s (1 thread:
-        // 2.2), 8 threads 11.5 -> 11.8.
+        // BB_CPU_PIN=1: every share on a pool thread pinned to its own CPU of
+        // the process's affinity set, the caller only waiting.  Off by
+        // default: on 8 container cores (2 048 worlds per thread) 2 threads
+        // 3.36 -> 3.97 M env-steps/s and 8 threads 11.5 -> 11.8, but on the
+        // GPU box's 16-core share 46.9 M pinned against 52-61 M unpinned in
+        // earlier runs (profiles/r03/final_bench.log).
         const char *pin = std::getenv("BB_CPU_PIN");
-        pinned_ = !(pin && *pin == '0') && n_ > 1;
+        pinned_ = pin && *pin == '1' && n_ > 1;
         cpu_set_t allowed;
         CPU_ZERO(&allowed);
         if (pinned_ && sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
