@@ -168,6 +168,25 @@ def test_gpu_policy_equals_host_and_torch(native_lib, stochastic):
 
 
 @pytest.mark.gpu
+def test_gpu_policy_multi_tile_waves_equal_host(native_lib):
+    """Every agent's rows (131 072 > 1 024 tiles of 64): each persistent wave
+    runs two tiles, the second tile's rows loaded under the first's network;
+    bit-identical to the host policy."""
+    assert torch.cuda.is_available()
+    sim, obs_all = real_obs(ExecMode.CUDA, W=65536, steps=60)
+    pol_g = FusedPolicy.from_agent(RefAgent(seed=4).cuda())
+    pol_h = pol_g.to("cpu")
+    obs = obs_all.reshape(-1, obs_all.shape[-1])
+    for stochastic in (False, True):
+        ag, lpg, vg = pol_g(obs, stochastic=stochastic, seed=5, step=3)
+        ah, lph, vh = pol_h(obs.cpu(), stochastic=stochastic, seed=5, step=3)
+        torch.cuda.synchronize()
+        assert torch.equal(ag.cpu(), ah)
+        assert torch.equal(lpg.cpu().view(torch.int32), lph.view(torch.int32))
+        assert torch.equal(vg.cpu().view(torch.int32), vh.view(torch.int32))
+
+
+@pytest.mark.gpu
 def test_gpu_policy_act_in_the_loop(native_lib):
     """env.py's loop with the fused policy writing the trainee's actions:
     device run == host run of the same loop, bit for bit."""
