@@ -135,6 +135,9 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="start the process group (RCCL on the GPU) even at world size 1: exercises the "
                          "multi-rank barrier / max-reduce path on one device")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="process-group backend on the GPU (nccl = RCCL; gloo only to rehearse the "
+                         "multi-rank path with several ranks sharing one GPU)")
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
@@ -151,7 +154,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     on_gpu = args.exec == "cuda"
     if on_gpu:
-        torch.cuda.set_device(local_rank if world_size > 1 else 0)
+        # (ranks beyond the node's GPUs share them round-robin: a rehearsal of
+        # the multi-rank path on a smaller box, with --dist-backend gloo)
+        torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()) if world_size > 1 else 0)
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
@@ -160,7 +165,10 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         if on_gpu:
-            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world_size)
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world_size)
+            else:
+                dist.init_process_group("gloo", rank=rank, world_size=world_size)
         else:
             dist.init_process_group("gloo", rank=rank, world_size=world_size)
 
@@ -188,7 +196,8 @@ def main():
     def max_over_ranks(x: float) -> float:
         if not use_dist:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        gloo = not on_gpu or args.dist_backend == "gloo"
+        t = torch.tensor([x], dtype=torch.float64, device="cpu" if gloo else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
