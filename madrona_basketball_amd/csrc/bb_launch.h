@@ -103,6 +103,7 @@ hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, in
 // synthetic action rows of its own worlds.
 class HostPool;
 int host_step(int n, const Params &p, HostPool &pool, bool actions = false, uint32_t seed = 0, uint32_t step = 0);
+int host_steps(int n, const Params &p, HostPool &pool, int32_t steps, bool actions, uint32_t seed, uint32_t step0);
 int host_init(int n, const Params &p);
 int host_random_actions(int n, const Params &p, HostPool &pool, uint32_t seed, uint32_t step);
 
