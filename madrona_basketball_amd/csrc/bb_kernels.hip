@@ -1144,6 +1144,84 @@ __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, c
     }
 }
 
+// ------------------------------------------------------------------ split step
+// One step over two waves per 32 worlds (small grids, N = 2): the sim wave S
+// loads the worlds, runs systems 1-17 and hands each lane's view of its world
+// to the observation wave O through LDS (SplitView, as k_rollout_split); O
+// writes the observation rows while S runs the reward and stores the state
+// columns, so the step costs load + systems + max(reward + stores, rows)
+// instead of their sum.  Same system, reward, store and row code on the same
+// inputs as k_step: bit-identical.
+template <int N>
+__global__ __launch_bounds__(2 * WAVE, 1) void k_step_split(const Params p)
+{
+    if constexpr (FusedRollout<N>::value) {
+        using T = StepTile<N, false>;
+        __shared__ SplitView<N> view;
+        __shared__ float4 tile4[T::FLOATS / 4];
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        const int lane = (int)threadIdx.x % WAVE;
+        const int k = lane % N;
+        const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+        const int64_t w = w0 + lane / N;
+        const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
+        if (wave == 0) {
+            const LaneAgents<N, MODE_FULL> ag{k, &p};
+            Ctx c = make_ctx(p, w, k == 0);
+            World<N> s, v;
+            LaneOrig x;
+            int32_t ib = -1;
+            bool share = false;
+            if (active) {
+                load_world(s, p, w);
+                Orig<N> o;
+                capture(o, s);
+                x.world = world_orig(o);
+                x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
+                step_world_pre_obs(s, c, ag);
+                agent_view(s, v, k);
+                ib = inbounder_id(s);
+                share = obs_sharable(s);
+                uint32_t u[SplitView<N>::WORDS];
+                __builtin_memcpy(u, &v, sizeof(World<N>));
+                u[SplitView<N>::WORDS - 2] = (uint32_t)ib;
+                u[SplitView<N>::WORDS - 1] = share ? 1u : 0u;
+#pragma unroll
+                for (int i = 0; i < SplitView<N>::WORDS; i++) view.w[i][lane] = u[i];
+            }
+            lds_barrier();  // the views are in LDS
+            if (active) {
+                sys_reward_agent(v, 0, AGENT0_ID + k);
+                store_world_agent<N, BB_COL_AUX>(v, p, w * N + k, 0, &x.agent);
+                if (k == 0) {
+                    Orig<N> o;
+                    set_world_orig(o, x.world);
+                    store_world_shared<N, BB_COL_AUX>(s, p, w, &o);
+                }
+            }
+        } else {
+            lds_barrier();  // the views are in LDS
+            World<N> v;
+            int32_t ib = -1;
+            bool share = false;
+            if (active) {
+                uint32_t u[SplitView<N>::WORDS];
+#pragma unroll
+                for (int i = 0; i < SplitView<N>::WORDS; i++) u[i] = view.w[i][lane];
+                __builtin_memcpy(&v, u, sizeof(World<N>));
+                ib = (int32_t)u[SplitView<N>::WORDS - 2];
+                share = u[SplitView<N>::WORDS - 1] != 0u;
+            }
+            const Ctx c = make_ctx(p, w, k == 0);
+            float *tile = (float *)tile4;
+            wide_obs_pass<N, 0, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+            wave_sync();  // the tile is rewritten by the next pass
+            if constexpr (T::PH > 1) wide_obs_pass<N, 1, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+            static_assert(T::PH <= 2, "two row passes");
+        }
+    }
+}
+
 // ------------------------------------------------------------------ PPO rollout
 // scripts/ppo.py:61-141 in one launch (bb_rollout_policy, N = 2): a workgroup
 // of 1 + PPO_PWAVES waves per 32 worlds.  Wave S holds the worlds in
@@ -2063,6 +2141,26 @@ bool step_wide(int64_t num_worlds)
 }
 
 // Compute units of the current device (256 on MI355X).
+static unsigned device_cus();
+
+// k_step_split (N = 2) while the step has at most this many worlds;
+// MADRONA_BB_STEP_SPLIT_MAX_WORLDS overrides it (0: never).
+#ifndef BB_STEP_SPLIT_MAX_WORLDS
+#define BB_STEP_SPLIT_MAX_WORLDS 0
+#endif
+template <int N>
+bool step_split(int64_t num_worlds)
+{
+    if constexpr (N == 2 && FusedRollout<N>::value && BB_STEP_BLOCKS == 1) {
+        const char *e = getenv("MADRONA_BB_STEP_SPLIT_MAX_WORLDS");  // read per launch (tests run both)
+        const int64_t mx = e && *e ? atoll(e) : BB_STEP_SPLIT_MAX_WORLDS;
+        return num_worlds <= mx;
+    } else {
+        return false;
+    }
+}
+
+// Compute units of the current device (256 on MI355X).
 static unsigned device_cus()
 {
     static const unsigned v = [] {
@@ -2085,7 +2183,9 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
     case MODE_FULL:
-        if (step_wide<N>(p.num_worlds))
+        if (step_split<N>(p.num_worlds))
+            hipExtLaunchKernelGGL(k_step_split<N>, grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p);
+        else if (step_wide<N>(p.num_worlds))
             hipExtLaunchKernelGGL(k_step_wide<N>, grid, dim3(WAVE * Wide<N>::WAVES), 0, s, ev0, ev1, 0, p);
         else if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid_full, block, 0, s, ev0, ev1, 0, p);
         else hipExtLaunchKernelGGL(k_step<N, MODE_FULL>, grid_full, block, 0, s, ev0, ev1, 0, p);

@@ -234,3 +234,24 @@ def test_gpu_sharded_worlds_concatenate_to_the_unsharded_run(agents, W):
         assert torch.equal(cat.view(torch.int32), full._views[n].view(torch.int32)), n
     # and the game actually happened on both shards
     assert int(full._views["rng_counter"][:half].sum()) > 0 and int(full._views["rng_counter"][half:].sum()) > 0
+
+
+@pytest.mark.parametrize("W", [8190, 16384])
+@pytest.mark.parametrize("flags", [dict(), dict(tag_mask=False, one_on_one=False)])
+def test_gpu_split_step_equals_single_wave_step(monkeypatch, W, flags):
+    """k_step_split (a sim wave + an observation wave per 32 worlds) == k_step
+    (MADRONA_BB_STEP_SPLIT_MAX_WORLDS=0) on every column after every step
+    of a random rollout, reset events included."""
+    sims = []
+    for mx in ("1000000000", "0"):
+        monkeypatch.setenv("MADRONA_BB_STEP_SPLIT_MAX_WORLDS", mx)
+        sim = make_sim(ExecMode.CUDA, W, per_world_rng=True, **flags)
+        sims.append(sim)
+    a, b = sims
+    for t in range(0, 400, 50):
+        for sim, mx in ((a, "1000000000"), (b, "0")):
+            monkeypatch.setenv("MADRONA_BB_STEP_SPLIT_MAX_WORLDS", mx)
+            sim.step_n(50, random_actions=True, action_seed=9, step0=t)
+            torch.cuda.synchronize()
+        for name in a._views:
+            assert torch.equal(a._views[name], b._views[name]), (t, name)
