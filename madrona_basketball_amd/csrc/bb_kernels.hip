@@ -2226,8 +2226,8 @@ static bool rollout_split(unsigned groups)
 {
     const char *e = getenv("MADRONA_BB_ROLLOUT_SPLIT");  // read per launch: the tests run both kernels
     const int forced = e && *e ? atoi(e) : -1;
-    const bool on = forced >= 0 ? forced != 0 : BB_ROLLOUT_SPLIT != 0;
-    return on && groups <= 2u * device_cus();
+    if (forced >= 0) return forced != 0;
+    return BB_ROLLOUT_SPLIT != 0 && groups <= 2u * device_cus();
 }
 
 template <int N>
