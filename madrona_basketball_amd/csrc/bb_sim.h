@@ -185,10 +185,25 @@ BB_HD float uni(float x)
 #endif
 }
 BB_HD F3 uni(F3 a) { return f3(uni(a.x), uni(a.y), uni(a.z)); }
+// A kernel-argument value kept in a scalar register and opaque to the
+// optimiser (so that a chain of selects over a table is not folded back into
+// a per-lane indexed load), without uni()'s readfirstlane, which is
+// convergent and keeps every branch around it from being if-converted.
+BB_HD float sconst(float x)
+{
+    return x;
+}
+BB_HD F3 sconst(F3 a) { return f3(sconst(a.x), sconst(a.y), sconst(a.z)); }
 BB_HD Q4 uni(Q4 q)
 {
     Q4 r;
     r.w = uni(q.w); r.x = uni(q.x); r.y = uni(q.y); r.z = uni(q.z);
+    return r;
+}
+BB_HD Q4 sconst(Q4 q)
+{
+    Q4 r;
+    r.w = sconst(q.w); r.x = sconst(q.x); r.y = sconst(q.y); r.z = sconst(q.z);
     return r;
 }
 
@@ -513,8 +528,8 @@ BB_HD float sample_uniform(World<N> &s, Ctx &c, float lo, float hi)
 template <int N>
 BB_HD F3 hoop_pos(const Ctx &c, int h)
 {
-    const F3 h0 = uni(f3(c.p->hoop0[0], c.p->hoop0[1], c.p->hoop0[2]));
-    const F3 h1 = uni(f3(c.p->hoop1[0], c.p->hoop1[1], c.p->hoop1[2]));
+    const F3 h0 = sconst(f3(c.p->hoop0[0], c.p->hoop0[1], c.p->hoop0[2]));
+    const F3 h1 = sconst(f3(c.p->hoop1[0], c.p->hoop1[1], c.p->hoop1[2]));
     return sel(h == 0, h0, h1);
 }
 
@@ -532,7 +547,7 @@ BB_HD Q4 start_orientation_eval(int i)  // gen.cpp:196 / :277
 template <int N>
 BB_HD Q4 start_orientation(const Ctx &c, int i)
 {
-    return sel(i % 2 == 0, uni(c.p->start_q[0]), uni(c.p->start_q[1]));
+    return sel(i % 2 == 0, sconst(c.p->start_q[0]), sconst(c.p->start_q[1]));
 }
 
 // setupAgentPositions (src/helper.cpp:108-160); returns the ball holder id.
@@ -767,19 +782,23 @@ BB_HD MoveIn gather_move(const World<N> &s, int i)
 BB_HD MoveOut move_one(const MoveIn &in, const Params &p)
 {
     MoveOut o;
+    // the tables' values first, unconditionally (branch-free selects below)
+    const Q4 t0 = sconst(p.turn_q[0]), t1 = sconst(p.turn_q[1]);
+    float ts[8], tc[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) { ts[k] = sconst(p.mv_sin[k]); tc[k] = sconst(p.mv_cos[k]); }
     o.q = in.q;
-    if (in.rotate != 0) o.q = qmul(sel(in.rotate == 1, uni(p.turn_q[0]), uni(p.turn_q[1])), in.q);
+    if (in.rotate != 0) o.q = qmul(sel(in.rotate == 1, t0, t1), in.q);
     o.vel = in.vel; o.px = in.px; o.py = in.py;
     if (in.can_move == 0) return o;
     const int32_t m = in.angle;
-    float sn = uni(p.mv_sin[0]), cs = uni(p.mv_cos[0]);
-    if ((uint32_t)m < 8u) {
+    float sn = ts[0], cs = tc[0];
 #pragma unroll
-        for (int k = 1; k < 8; k++)
-            if (m == k) { sn = uni(p.mv_sin[k]); cs = uni(p.mv_cos[k]); }
-    } else {
-        bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
+    for (int k = 1; k < 8; k++) {
+        sn = m == k ? ts[k] : sn;
+        cs = m == k ? tc[k] : cs;
     }
+    if ((uint32_t)m >= 8u) bbm::sincosf_((float)m * ANGLE_STEP, &sn, &cs);
     F3 dv = (f3(sn, -cs, 0.f) * in.quickness) * (float)in.move;
     float maxs = in.max_speed;
     const F3 fw = forward(o.q);
