@@ -1746,19 +1746,27 @@ struct LaneSources {
     }
 };
 
-// The wave's rows [row0, row0 + WPW*N) whose bit is set in `rows`, row by
-// row: lane L writes pieces L, L + 64, ... of each row (the row's bytes in 1 KB
-// of consecutive pieces per store instruction).  A lane's pieces sit at the
-// same row positions in every row, so their table entries are decoded once,
-// per observer a (the row loop is unrolled over a), before the loop: per
-// piece the loop does 4 LDS reads and one store; the row's team (obs 0-22
-// entries) is a wave-uniform offset.
+// The wave's rows [row0, row0 + WPW*N) whose bit is set in `rows`: lane L
+// writes pieces L, L + 64, ... of each row (the row's bytes in 1 KB of
+// consecutive pieces per store instruction).  A lane's pieces sit at the same
+// row positions in every row, so their table entries are decoded once, per
+// observer a, before the loop: per piece 4 LDS reads and one store; the row's
+// team (obs 0-22 entries) is a wave-uniform offset.
+// The reads of RB rows are issued together, ahead of their stores (only the
+// stores are predicated on the row's bit): one LDS round trip per RB rows
+// instead of per row -- row by row, each row's store waited on its own reads
+// (N = 4: 64 round trips per wave, the observation phase 9-22 us per wave).
 // Slots [S0, S1) of the wave's worlds, whose sources are at sm.e[slot - S0].
+#ifndef BB_OBS_RB
+#define BB_OBS_RB 0  // rows per read batch (0: a slot's N rows at one piece per row, else 2)
+#endif
 template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
 __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
     constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
+    constexpr int RB = (BB_OBS_RB > 0 && N % BB_OBS_RB == 0) ? BB_OBS_RB : (NP == 1 ? N : 2);
+    static_assert(N % RB == 0, "whole read batches per slot");
     int src[NP][N][4], dtm[NP][4];
 #pragma unroll
     for (int p = 0; p < NP; p++) {
@@ -1776,18 +1784,30 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
     static_assert(S1 <= WPW && S1 - S0 <= SharedLds<N>::SPP, "part of the source table");
     for (int slot = S0; slot < S1; slot++) {
         const float *e = sm.e[slot - S0];
+        if (!((rows >> (slot * N)) & ((1ull << N) - 1))) continue;  // no row of this world (wave-uniform)
+        // team 1: all ones (as a mask whatever the entry holds: the table of a
+        // world whose rows are written directly is never filled in)
+        int tmask[N];
 #pragma unroll
-        for (int a = 0; a < N; a++) {
-            const int r = slot * N + a;
-            if (!((rows >> r) & 1ull)) continue;  // wave-uniform
-            const int tmask = -(int)fbits(e[esw(S::TM + a)]);  // team 1: all ones
+        for (int a = 0; a < N; a++) tmask[a] = fbits(e[esw(S::TM + a)]) != 0u ? -1 : 0;
 #pragma unroll
-            for (int p = 0; p < NP; p++) {
-                if (p * WAVE + lane < QR) {
-                    const float v0 = e[src[p][a][0] + (dtm[p][0] & tmask)], v1 = e[src[p][a][1] + (dtm[p][1] & tmask)];
-                    const float v2 = e[src[p][a][2] + (dtm[p][2] & tmask)], v3 = e[src[p][a][3] + (dtm[p][3] & tmask)];
-                    row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, vf4{v0, v1, v2, v3});
+        for (int a0 = 0; a0 < N; a0 += RB) {
+            vf4 v[RB][NP];
+#pragma unroll
+            for (int b = 0; b < RB; b++)
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    const int a = a0 + b, tm = tmask[a];
+                    v[b][p] = vf4{e[src[p][a][0] + (dtm[p][0] & tm)], e[src[p][a][1] + (dtm[p][1] & tm)],
+                                  e[src[p][a][2] + (dtm[p][2] & tm)], e[src[p][a][3] + (dtm[p][3] & tm)]};
                 }
+#pragma unroll
+            for (int b = 0; b < RB; b++) {
+                const int r = slot * N + a0 + b;
+                if (!((rows >> r) & 1ull)) continue;  // wave-uniform
+#pragma unroll
+                for (int p = 0; p < NP; p++)
+                    if (p * WAVE + lane < QR) row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, v[b][p]);
             }
         }
     }

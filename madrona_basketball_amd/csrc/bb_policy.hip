@@ -34,6 +34,16 @@ __device__ __forceinline__ void pol_trace(const PolicyArgs &a, bool first, int p
     }
 }
 
+// the same clocks for k_policy_wg, indexed by the wave's global id
+__device__ __forceinline__ void pol_trace_wg(const PolicyArgs &a, int64_t gw, int point, bool wait_mem)
+{
+    if (a.diag_ts) {
+        if (wait_mem) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = wall_clock64();
+        if ((threadIdx.x & 63) == 0) a.diag_ts[gw * POL_TRACE_POINTS + point] = t;
+    }
+}
+
 template <int MT>
 __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
 {
@@ -147,6 +157,201 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_policy_wg: the network's B operands in LDS, shared by a workgroup of up
+// to 12 waves (one workgroup per CU, three waves per SIMD),
+// 16-row tiles per wave in a grid-stride loop.  With the weights in
+// registers (k_policy) a wave needs 238-480 VGPRs, so a SIMD holds one or two
+// waves and each wave's chain -- row loads, 96 dependent-pair MFMAs, the
+// LayerNorm DPP trees, the bucket pass -- runs alone; here three waves per
+// SIMD overlap one wave's MFMAs with the others' VALU / LDS / memory work.
+// Every value is computed as k_policy<1> computes it (the same MFMA operands
+// in the same order, the same LayerNorm and bucket pass), so the outputs are
+// bit-identical.
+//
+// LDS images of the weights, conflict-free for the lanes' 16-byte reads
+// (lane (c, q) reads W[16t + c][k-chunk q]): planes [q][n][j] padded to 36 /
+// 12 floats (tools-free check: every ds_read_b128 lane group of 16 lanes
+// covers the 64 banks once).
+#ifndef BB_PWG_WAVES
+#define BB_PWG_WAVES 12  // 3 per SIMD: 141-159 VGPRs (at 16 the 128-VGPR budget spills 16-104 B)
+#endif
+constexpr int PWG_WAVES = BB_PWG_WAVES;
+constexpr int PWG_P1 = 36, PWG_P2 = 12;
+struct PolicyWgLds {
+    float w1[4][32][PWG_P1];  // W1[n][32q + j]
+    float w2[4][32][PWG_P2];  // W2[n][8q + j]
+    float wh[4][32][PWG_P2];  // head_w[n][8q + j]
+    float norm[2][POL_IN];
+    float cst[7][32];  // b1, ln1_w, ln1_b, b2, ln2_w, ln2_b, head_b (read at their use: no live registers)
+    float tile[PWG_WAVES][16][33];
+    BucketLds<16> bl[PWG_WAVES];
+};
+
+template <bool PREFETCH, int STOCH>
+__global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a)
+{
+    __shared__ __attribute__((aligned(16))) PolicyWgLds L;
+    const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63, c = lane & 15, q = lane >> 4;
+    const int nw = (int)(blockDim.x >> 6);
+    const int64_t tiles = (a.rows + 15) / 16;
+    const int64_t tw0 = (int64_t)blockIdx.x * nw + wave, tstride = (int64_t)gridDim.x * nw;
+    pol_trace_wg(a, tw0, 0, false);
+    const PolicyWeights &W = a.w;
+    // lane (c, q): observation floats 32q .. 32q + 31 of row row0 + c
+    auto load_rows = [&](int64_t row0, float (&x)[32]) {
+        const int64_t r = row0 + c;
+        if (r < a.rows) {
+            const float4 *src = (const float4 *)(a.obs + r * a.obs_stride + 32 * q);
+#pragma unroll
+            for (int v = 0; v < 8; v++) {
+                const float4 o = src[v];
+                x[4 * v] = o.x; x[4 * v + 1] = o.y; x[4 * v + 2] = o.z; x[4 * v + 3] = o.w;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 32; j++) x[j] = 0.f;
+        }
+    };
+    // the first tile's rows in flight under the weight copy
+    float xn[32];
+    if (tw0 < tiles) load_rows(tw0 * 16, xn);
+    for (int i = tid; i < 32 * 32; i += (int)blockDim.x) {  // W1 [32][128] as float4
+        const int n = i >> 5, k = 4 * (i & 31);
+        *(float4 *)&L.w1[k >> 5][n][k & 31] = ((const float4 *)W.w1)[i];
+    }
+    for (int i = tid; i < 32 * 8; i += (int)blockDim.x) {  // W2, head_w [32][32] as float4
+        const int n = i >> 3, k = 4 * (i & 7);
+        *(float4 *)&L.w2[k >> 3][n][k & 7] = ((const float4 *)W.w2)[i];
+        *(float4 *)&L.wh[k >> 3][n][k & 7] = ((const float4 *)W.head_w)[i];
+    }
+    for (int k = tid; k < POL_IN; k += (int)blockDim.x) {
+        L.norm[0][k] = W.obs_mean[k];
+        L.norm[1][k] = W.obs_inv[k];
+    }
+    for (int k = tid; k < 7 * 32; k += (int)blockDim.x) {
+        const float *src[7] = {W.b1, W.ln1_w, W.ln1_b, W.b2, W.ln2_w, W.ln2_b, W.head_b};
+        L.cst[k >> 5][k & 31] = src[k >> 5][k & 31];
+    }
+    __syncthreads();
+    pol_trace_wg(a, tw0, 1, true);
+    float (*tile)[33] = L.tile[wave];
+
+    for (int64_t tl = tw0; tl < tiles; tl += tstride) {
+        const int64_t row0 = tl * 16;
+        const bool first = tl == tw0;
+        float x[32];
+#pragma unroll
+        for (int j = 0; j < 32; j++) x[j] = xn[j];
+        if (PREFETCH && tl + tstride < tiles) load_rows((tl + tstride) * 16, xn);
+        if (a.obs_out) {  // the rollout's record of the observed rows (buffer.obs, ppo.py:129)
+            const int64_t r = row0 + c;
+            if (r < a.rows) {
+                float4 *dst = (float4 *)(a.obs_out + r * POL_IN + 32 * q);
+#pragma unroll
+                for (int v = 0; v < 8; v++) dst[v] = make_float4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
+            }
+        }
+        if (first) pol_trace_wg(a, tw0, 2, true);
+        // an offset the compiler cannot see through: the LDS operand reads stay
+        // inside the loop instead of being hoisted into 128 live registers
+        int z = 0;
+        __asm__ volatile("" : "+v"(z));
+        const float (*nrm)[POL_IN] = (const float (*)[POL_IN])(&L.norm[0][0] + z);
+        const float (*w1l)[32][PWG_P1] = (const float (*)[32][PWG_P1])(&L.w1[0][0][0] + z);
+        const float (*w2l)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.w2[0][0][0] + z);
+        const float (*whl)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.wh[0][0][0] + z);
+        const float (*cs)[32] = (const float (*)[32])(&L.cst[0][0] + z);
+        // layer 1: normalisation, then the two accumulator chains (policy_layers).
+        // The LDS operands are read one 4-float group ahead of their use and the
+        // groups fenced with scheduling barriers: hoisted all at once they would
+        // take 64 more registers (spills at four waves per SIMD).
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float4 m4 = *(const float4 *)&nrm[0][32 * q + 4 * v];
+            const float4 i4 = *(const float4 *)&nrm[1][32 * q + 4 * v];
+            x[4 * v] = pol_clamp((x[4 * v] - m4.x) * i4.x);
+            x[4 * v + 1] = pol_clamp((x[4 * v + 1] - m4.y) * i4.y);
+            x[4 * v + 2] = pol_clamp((x[4 * v + 2] - m4.z) * i4.z);
+            x[4 * v + 3] = pol_clamp((x[4 * v + 3] - m4.w) * i4.w);
+            if (v & 1) __builtin_amdgcn_sched_barrier(0);
+        }
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+        float4 n0 = *(const float4 *)&w1l[q][c][0], n1 = *(const float4 *)&w1l[q][16 + c][0];
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const float w0[4] = {n0.x, n0.y, n0.z, n0.w}, w1[4] = {n1.x, n1.y, n1.z, n1.w};
+            if (v + 1 < 8) {
+                n0 = *(const float4 *)&w1l[q][c][4 * v + 4];
+                n1 = *(const float4 *)&w1l[q][16 + c][4 * v + 4];
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[4 * v + e], w0[e], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[4 * v + e], w1[e], a1, 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        ln_relu_to_tile(a0, a1, cs[0][c], cs[0][c + 16], cs[1][c], cs[1][c + 16], cs[2][c], cs[2][c + 16], tile, c, q);
+        pol_wave_sync();
+        // layer 2, then the heads (k = 8q + j)
+#pragma unroll
+        for (int layer = 0; layer < 2; layer++) {
+            const float (*wl)[32][PWG_P2] = layer == 0 ? w2l : whl;
+            float h[8];
+#pragma unroll
+            for (int j = 0; j < 8; j++) h[j] = tile[c][8 * q + j];
+            pol_wave_sync();
+            float w0[8], w1[8];
+#pragma unroll
+            for (int v = 0; v < 2; v++) {
+                const float4 u0 = *(const float4 *)&wl[q][c][4 * v];
+                const float4 u1 = *(const float4 *)&wl[q][16 + c][4 * v];
+                w0[4 * v] = u0.x; w0[4 * v + 1] = u0.y; w0[4 * v + 2] = u0.z; w0[4 * v + 3] = u0.w;
+                w1[4 * v] = u1.x; w1[4 * v + 1] = u1.y; w1[4 * v + 2] = u1.z; w1[4 * v + 3] = u1.w;
+            }
+            a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+            a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w0[j], a0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w1[j], a1, 0, 0, 0);
+            }
+            if (layer == 0) {
+                ln_relu_to_tile(a0, a1, cs[3][c], cs[3][c + 16], cs[4][c], cs[4][c + 16], cs[5][c], cs[5][c + 16], tile, c, q);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    tile[4 * q + i][c] = a0[i] + cs[6][c];
+                    tile[4 * q + i][c + 16] = a1[i] + cs[6][c + 16];
+                }
+            }
+            pol_wave_sync();
+        }
+        if (first) pol_trace_wg(a, tw0, 4, false);
+        bucket_pass_spread<16, false, STOCH>(a, tile, row0, lane, L.bl[wave]);
+        pol_wave_sync();
+        if (first) pol_trace_wg(a, tw0, 5, false);
+    }
+}
+
+// Waves per workgroup and workgroups of a k_policy_wg launch: one workgroup
+// per CU (256) once there are 12 tiles per CU, fewer waves per workgroup
+// below that so that every CU gets work.
+struct PolicyWgGrid {
+    int waves;
+    unsigned groups;
+};
+inline PolicyWgGrid policy_wg_grid(int64_t tiles)
+{
+    constexpr int64_t CUS = 256;
+    int64_t w = (tiles + CUS - 1) / CUS;
+    w = w < 1 ? 1 : (w > PWG_WAVES ? PWG_WAVES : w);
+    int64_t g = (tiles + w - 1) / w;
+    g = g > CUS ? CUS : g;
+    return {(int)w, (unsigned)g};
+}
+
 // M-tiles per wave.  4: 64 rows per wave, one row per lane in the bucket
 // pass, each lane's 19 Gumbel draws in series; 1: 16 rows per wave, 4 lanes
 // per row in the bucket pass.  Measured (profiles/r03/e_policy_mt_ab.txt):
@@ -187,8 +392,43 @@ static hipError_t launch_policy_mt(const PolicyArgs &a, hipStream_t s)
     return hipGetLastError();
 }
 
+// k_policy_wg from POLICY_WG_MIN_ROWS rows on: measured (profiles/r03/ap_policy_ab.txt)
+// 131 072 rows 43.2 -> 38.4 us argmax, 53.9 -> 49.1 sampled; at 65 536 rows the
+// register-weight kernel is ahead (25.3 vs 27.1, 30.3 vs 34.3: its 64-row
+// tiles amortise the bucket pass's per-tile exchanges).  MADRONA_BB_POLICY_WG=1 / 0
+// forces it on / off; MADRONA_BB_POLICY_MT forces a register-weight kernel.
+#ifndef POLICY_WG_MIN_ROWS
+#define POLICY_WG_MIN_ROWS 98304
+#endif
+static bool policy_wg_enabled(int64_t rows)
+{
+    static const int forced = [] {
+        const char *e = getenv("MADRONA_BB_POLICY_WG");
+        const char *m = getenv("MADRONA_BB_POLICY_MT");
+        if (m && *m) return 0;
+        return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
+    }();
+    return forced >= 0 ? forced == 1 : rows >= POLICY_WG_MIN_ROWS;
+}
+
 hipError_t launch_policy(const PolicyArgs &a, hipStream_t s)
 {
+    if (policy_wg_enabled(a.rows)) {
+        const int64_t tiles = (a.rows + 15) / 16;
+        if (tiles <= 0) return hipSuccess;
+        const PolicyWgGrid g = policy_wg_grid(tiles);
+        // the next tile's rows under this one's network once a wave has two
+        const bool pre = tiles > (int64_t)g.groups * g.waves;
+        const dim3 grid(g.groups), block(64 * g.waves);
+        if (a.stochastic) {
+            if (pre) hipLaunchKernelGGL((k_policy_wg<true, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_policy_wg<false, 1>), grid, block, 0, s, a);
+        } else {
+            if (pre) hipLaunchKernelGGL((k_policy_wg<true, 0>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_policy_wg<false, 0>), grid, block, 0, s, a);
+        }
+        return hipGetLastError();
+    }
     switch (policy_mt(a.rows)) {
     case 1: return launch_policy_mt<1>(a, s);
     case 2: return launch_policy_mt<2>(a, s);

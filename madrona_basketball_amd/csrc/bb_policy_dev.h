@@ -123,7 +123,8 @@ __device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
 }
 // PRE (compile-time, so that the noise stays in registers: a runtime-null
 // pointer to it would put it in scratch): `pre` holds this lane's noise.
-template <int R, bool PRE = false>
+// STOCH: -1 a.stochastic at run time, 0 / 1 fixed at compile time.
+template <int R, bool PRE = false, int STOCH = -1>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
                                                    BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr,
                                                    const BucketNoise<R> *pre = nullptr, uint64_t *ts = nullptr)
@@ -136,7 +137,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     const int r = lane / LPR, part = lane % LPR;
     const int64_t rr = row0 + r;
     const bool live = rr < a.rows;
-    const bool stochastic = a.stochastic != 0;
+    const bool stochastic = STOCH < 0 ? a.stochastic != 0 : STOCH == 1;
     const float *lg = tile[r];
     // bucket maxima (every lane, compile-time indices)
     float mx[POL_BUCKETS];
