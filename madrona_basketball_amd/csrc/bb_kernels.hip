@@ -1750,18 +1750,59 @@ struct LaneSources {
 // writes pieces L, L + 64, ... of each row (the row's bytes in 1 KB of
 // consecutive pieces per store instruction).  A lane's pieces sit at the same
 // row positions in every row, so their table entries are decoded once, per
-// observer a, before the loop: per piece 4 LDS reads and one store; the row's
-// team (obs 0-22 entries) is a wave-uniform offset.
-// The reads of RB rows are issued together, ahead of their stores (only the
-// stores are predicated on the row's bit): one LDS round trip per RB rows
-// instead of per row -- row by row, each row's store waited on its own reads
-// (N = 4: 64 round trips per wave, the observation phase 9-22 us per wave).
+// observer a, before the loop: per piece 4 LDS reads and one store.  The
+// row's team (obs 0-22 entries) is bit r of `teams` (a ballot taken when the
+// sources were computed): a wave-uniform offset with no LDS read.
+// Rows go in read batches of RB rows; the reads of the next batch are issued
+// before this batch's stores (only the stores are predicated on the row's
+// bit), so the LDS latency hides under the stores -- row by row, each row's
+// store waited on its own reads (and on a read of its team before them).
 // Slots [S0, S1) of the wave's worlds, whose sources are at sm.e[slot - S0].
 #ifndef BB_OBS_RB
 #define BB_OBS_RB 0  // rows per read batch (0: a slot's N rows at one piece per row, else 2)
 #endif
+template <int N, int NP, int RB, int A0>
+__device__ __forceinline__ void read_batch(const float *e, const int (&src)[NP][N][4], const int (&dtm)[NP][4],
+                                           uint64_t tbits, vf4 (&v)[RB][NP])
+{
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+        const int tm = -(int)((tbits >> (A0 + b)) & 1ull);  // team 1: all ones
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+            v[b][p] = vf4{e[src[p][A0 + b][0] + (dtm[p][0] & tm)], e[src[p][A0 + b][1] + (dtm[p][1] & tm)],
+                          e[src[p][A0 + b][2] + (dtm[p][2] & tm)], e[src[p][A0 + b][3] + (dtm[p][3] & tm)]};
+    }
+}
+template <int N, int AUX, int S0, int S1, int NP, int RB, int A0>
+__device__ __forceinline__ void emit_slot_batches(const SharedLds<N> &sm, const int (&src)[NP][N][4],
+                                                  const int (&dtm)[NP][4], uint64_t rows, uint64_t teams, char *base,
+                                                  int lane, int slot, vf4 (&cur)[RB][NP])
+{
+    constexpr int QR = ObsSrc<N>::QR;
+    vf4 nxt[RB][NP];
+    if constexpr (A0 + RB < N) {
+        read_batch<N, NP, RB, A0 + RB>(sm.e[slot - S0], src, dtm, teams >> (slot * N), nxt);
+    } else {
+        if (slot + 1 < S1) read_batch<N, NP, RB, 0>(sm.e[slot + 1 - S0], src, dtm, teams >> ((slot + 1) * N), nxt);
+    }
+#pragma unroll
+    for (int b = 0; b < RB; b++) {
+        const int r = slot * N + A0 + b;
+        if (!((rows >> r) & 1ull)) continue;  // wave-uniform
+#pragma unroll
+        for (int p = 0; p < NP; p++)
+            if (p * WAVE + lane < QR) row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, cur[b][p]);
+    }
+#pragma unroll
+    for (int b = 0; b < RB; b++)
+#pragma unroll
+        for (int p = 0; p < NP; p++) cur[b][p] = nxt[b][p];
+    if constexpr (A0 + RB < N) emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB>(sm, src, dtm, rows, teams, base, lane, slot, cur);
+}
 template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
-__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, float *obs, int64_t row0, int lane)
+__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+                                            int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
     constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
@@ -1782,42 +1823,17 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
     }
     char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
     static_assert(S1 <= WPW && S1 - S0 <= SharedLds<N>::SPP, "part of the source table");
-    for (int slot = S0; slot < S1; slot++) {
-        const float *e = sm.e[slot - S0];
-        if (!((rows >> (slot * N)) & ((1ull << N) - 1))) continue;  // no row of this world (wave-uniform)
-        // team 1: all ones (as a mask whatever the entry holds: the table of a
-        // world whose rows are written directly is never filled in)
-        int tmask[N];
-#pragma unroll
-        for (int a = 0; a < N; a++) tmask[a] = fbits(e[esw(S::TM + a)]) != 0u ? -1 : 0;
-#pragma unroll
-        for (int a0 = 0; a0 < N; a0 += RB) {
-            vf4 v[RB][NP];
-#pragma unroll
-            for (int b = 0; b < RB; b++)
-#pragma unroll
-                for (int p = 0; p < NP; p++) {
-                    const int a = a0 + b, tm = tmask[a];
-                    v[b][p] = vf4{e[src[p][a][0] + (dtm[p][0] & tm)], e[src[p][a][1] + (dtm[p][1] & tm)],
-                                  e[src[p][a][2] + (dtm[p][2] & tm)], e[src[p][a][3] + (dtm[p][3] & tm)]};
-                }
-#pragma unroll
-            for (int b = 0; b < RB; b++) {
-                const int r = slot * N + a0 + b;
-                if (!((rows >> r) & 1ull)) continue;  // wave-uniform
-#pragma unroll
-                for (int p = 0; p < NP; p++)
-                    if (p * WAVE + lane < QR) row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, v[b][p]);
-            }
-        }
-    }
+    vf4 cur[RB][NP];
+    read_batch<N, NP, RB, 0>(sm.e[0], src, dtm, teams >> (S0 * N), cur);
+    for (int slot = S0; slot < S1; slot++)
+        emit_slot_batches<N, AUX, S0, S1, NP, RB, 0>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
 
 // The source table written and emitted part by part (BB_OBS_PARTS): the
 // world state is dead once every lane holds its sources; each part's lanes
 // put theirs, the wave emits that part's rows, and the next part overlays it.
 template <int N, int AUX, int P = 0>
-__device__ __forceinline__ void obs_parts(SharedLds<N> &sm, const LaneSources<N> &src, uint64_t rows, float *obs,
+__device__ __forceinline__ void obs_parts(SharedLds<N> &sm, const LaneSources<N> &src, uint64_t rows, uint64_t teams, float *obs,
                                           int64_t row0, int lane, int slot, int k, bool active, bool share)
 {
     using SL = SharedLds<N>;
@@ -1825,8 +1841,8 @@ __device__ __forceinline__ void obs_parts(SharedLds<N> &sm, const LaneSources<N>
     __syncthreads();  // the world state (or the previous part) is dead: this part overlays it
     if (active && slot >= S0 && slot < S1) src.put(sm.e[slot - S0], k, share);
     __syncthreads();
-    emit_pieces<N, AUX, S0, S1>(sm, rows, obs, row0, lane);
-    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1>(sm, src, rows, obs, row0, lane, slot, k, active, share);
+    emit_pieces<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
+    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1>(sm, src, rows, teams, obs, row0, lane, slot, k, active, share);
 }
 
 template <int N, int MODE, int PHASE = 0>
@@ -1946,9 +1962,10 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
             }
         }
         const uint64_t rows = __ballot(active && share);
+        const uint64_t teams = __ballot(active && share && src.tm != 0);  // bit r: row r's observer in team 1
         // the row pass (memory-bound) ahead of other waves' systems (VALU)
         if constexpr (BB_PRIO_ROWS > 0) __builtin_amdgcn_s_setprio(BB_PRIO_ROWS);
-        obs_parts<N, AUX>(sm, src, rows, p.c.obs, w0 * N, lane, slot, k, active, share);
+        obs_parts<N, AUX>(sm, src, rows, teams, p.c.obs, w0 * N, lane, slot, k, active, share);
         trace_point<MODE>(p, 9);
         return;
     }
