@@ -1800,9 +1800,9 @@ __device__ __forceinline__ void emit_slot_batches(const SharedLds<N> &sm, const 
         for (int p = 0; p < NP; p++) cur[b][p] = nxt[b][p];
     if constexpr (A0 + RB < N) emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
-template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
-__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
-                                            int64_t row0, int lane)
+template <int N, int AUX, int S0, int S1>
+__device__ __forceinline__ void emit_pieces_rows(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+                                                 int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
     constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
@@ -1827,6 +1827,79 @@ __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t row
     read_batch<N, NP, RB, 0>(sm.e[0], src, dtm, teams >> (S0 * N), cur);
     for (int slot = S0; slot < S1; slot++)
         emit_slot_batches<N, AUX, S0, S1, NP, RB, 0>(sm, src, dtm, rows, teams, base, lane, slot, cur);
+}
+
+// Row groups as one stretch of pieces (BB_OBS_FLAT): a group of G
+// consecutive rows of one world is G * QR consecutive 16-byte pieces, written
+// by ceil(G * QR / 64) whole-wave store instructions -- instruction i, lane L:
+// piece 64 i + L of the group -- instead of ceil(QR / 64) per row (N = 4:
+// 46 of 64 lanes per row; N = 10: 64 + 42).  A lane's pieces are then at
+// different row positions (row 64 i + L div QR of the group), decoded once
+// per instruction slot i and per group of the world (the observer is
+// g G + that row), before the loop.
+#ifndef BB_OBS_FLAT
+#define BB_OBS_FLAT 0  // measured slower (profiles/r03/ar_*): N = 4 63.9-65.5 vs 63.5-64.4 us, N = 10 293-294 vs 285-288
+#endif
+template <int N>
+struct FlatGroups {
+    static constexpr int QR = ObsSrc<N>::QR;
+    static constexpr int G = N <= 4 ? N : N / 2;  // rows per group
+    static constexpr int NG = N / G;               // groups per world
+    static constexpr int GQ = G * QR;              // pieces per group
+    static constexpr int INS = (GQ + WAVE - 1) / WAVE;
+    static_assert(N % G == 0, "whole groups per world");
+};
+template <int N, int AUX, int S0, int S1>
+__device__ __forceinline__ void emit_pieces_flat(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+                                                 int64_t row0, int lane)
+{
+    using F = FlatGroups<N>;
+    constexpr int QR = F::QR, G = F::G, NG = F::NG, GQ = F::GQ, INS = F::INS;
+    int src[NG][INS][4], dtm[INS][4], rg[INS];
+#pragma unroll
+    for (int i = 0; i < INS; i++) {
+        const int f = i * WAVE + lane;
+        const bool ok = f < GQ;
+        const int r = ok ? f / QR : 0, q = ok ? f - r * QR : 0;
+        rg[i] = ok ? r : 63;  // 63: no row (the row bits above G are cleared below)
+        const uint4 cd = sm.code[q];
+        const uint32_t code[4] = {cd.x, cd.y, cd.z, cd.w};
+#pragma unroll
+        for (int c = 0; c < 4; c++) {
+#pragma unroll
+            for (int g = 0; g < NG; g++) src[g][i][c] = esw(piece_src<N>(code[c], g * G + r, 0));
+            dtm[i][c] = esw(piece_src<N>(code[c], 0, 1)) - esw(piece_src<N>(code[c], 0, 0));  // context entries only
+        }
+    }
+    char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
+    constexpr uint64_t GMASK = (1ull << G) - 1;
+    for (int slot = S0; slot < S1; slot++) {
+        const float *e = sm.e[slot - S0];
+#pragma unroll
+        for (int g = 0; g < NG; g++) {
+            const int r0 = slot * N + g * G;
+            const uint64_t gm = (rows >> r0) & GMASK, gt = (teams >> r0) & GMASK;
+            if (!gm) continue;  // wave-uniform
+            vf4 v[INS];
+#pragma unroll
+            for (int i = 0; i < INS; i++) {
+                const int tm = -(int)((gt >> rg[i]) & 1ull);  // team 1: all ones
+                v[i] = vf4{e[src[g][i][0] + (dtm[i][0] & tm)], e[src[g][i][1] + (dtm[i][1] & tm)],
+                           e[src[g][i][2] + (dtm[i][2] & tm)], e[src[g][i][3] + (dtm[i][3] & tm)]};
+            }
+            const uint32_t off0 = (uint32_t)r0 * QR * 16u;
+#pragma unroll
+            for (int i = 0; i < INS; i++)
+                if ((gm >> rg[i]) & 1ull) row_store<AUX>(base, off0 + (uint32_t)(i * WAVE + lane) * 16u, v[i]);
+        }
+    }
+}
+template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
+__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+                                            int64_t row0, int lane)
+{
+    if constexpr (BB_OBS_FLAT) emit_pieces_flat<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
+    else emit_pieces_rows<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
 }
 
 // The source table written and emitted part by part (BB_OBS_PARTS): the
