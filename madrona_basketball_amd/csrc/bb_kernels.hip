@@ -1806,7 +1806,7 @@ __device__ __forceinline__ void emit_pieces_rows(const SharedLds<N> &sm, uint64_
 {
     using S = ObsSrc<N>;
     constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
-    constexpr int RB = (BB_OBS_RB > 0 && N % BB_OBS_RB == 0) ? BB_OBS_RB : (NP == 1 ? N : 2);
+    constexpr int RB = (BB_OBS_RB > 0 && N % (BB_OBS_RB > 0 ? BB_OBS_RB : 1) == 0) ? BB_OBS_RB : (NP == 1 ? N : 2);
     static_assert(N % RB == 0, "whole read batches per slot");
     int src[NP][N][4], dtm[NP][4];
 #pragma unroll
