@@ -17,7 +17,7 @@
  *   bb_fill_random_actions <- (new) stages a_k for bb_step_n_staged
  *   bb_rollout          <- n x (actions[:] = a_k; Manager::step; copy of
  *                          observations/rewards/dones), the rollout loop of
- *                          scripts/ppo.py:139-176 with a_k staged in HBM
+ *                          scripts/ppo.py:61-141 with a_k staged in HBM
  *   bb_record           <- the per-step trajectory logging of scripts/ppo.py:93-106
  *                          and scripts/infer.py:116-129 (ten .cpu() copies per
  *                          step), as one device-side copy into a ring
@@ -240,7 +240,7 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
  * Sampling as bb_policy_forward with step = step0 + k (stochastic = 0: argmax);
  * the opponent samples with seed ^ 0x9E3779B9.  Equal, bit for bit, to n x
  * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
- * On gfx950 without an opponent (and up to 8 192 worlds) one fused launch
+ * On gfx950 without an opponent (and up to 16 384 worlds) one fused launch
  * runs all n steps; flags BB_ROLLOUT_PER_STEP forces a policy launch and a
  * step launch per step instead.
  * kernel_ms (CUDA mode): time from the first launch to the last, after a sync. */

@@ -4,8 +4,14 @@
 #include <hip/hip_runtime.h>
 #include "bb_launch.h"
 #include "bb_rng.h"
+#include <cstdlib>
 
 namespace bb {
+
+int force_rollout_split = [] {
+    const char *e = std::getenv("MADRONA_BB_ROLLOUT_SPLIT");
+    return e && *e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+}();
 
 // one lane = one (world, agent) action row (24 B); N compile-time so the
 // row -> (world, agent) split is a multiply, not a 64-bit division

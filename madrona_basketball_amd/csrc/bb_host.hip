@@ -854,6 +854,17 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
 
 namespace {
 
+// Start / end events of a timed region, destroyed on every exit path.
+struct EventPair {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    bool create() { return hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess; }
+    ~EventPair()
+    {
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }
+};
+
 bool weights_ok(const bb_policy_weights *w)
 {
     if (!w) return false;
@@ -952,13 +963,16 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         if (final_needed) bb::host_policy(pass(n, true));
         return BB_OK;
     }
+    // the kernels store obs rows as float4 and action rows as int2
+    const auto misaligned = [](const void *ptr, uintptr_t a) { return ptr && ((uintptr_t)ptr & (a - 1)) != 0; };
+    if (misaligned(out->obs, 16) || misaligned(out->actions, 8))
+        return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy: out->obs must be 16-byte and out->actions 8-byte aligned");
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
+    EventPair ev;  // destroyed on every exit
     if (kernel_ms) {
-        if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess)
-            return fail(BB_ERR_HIP, "hipEventCreate");
-        (void)hipEventRecord(e0, st);
+        if (!ev.create()) return fail(BB_ERR_HIP, "hipEventCreate");
+        (void)hipEventRecord(ev.e0, st);
     }
     const bool fused = !(flags & BB_ROLLOUT_PER_STEP) && !opponent && bb::fused_rollout_n(s->n) &&
                        W <= ppo_fused_max_worlds();
@@ -1007,12 +1021,10 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
     }
     if (kernel_ms) {
-        (void)hipEventRecord(e1, st);
-        hipError_t e = hipEventSynchronize(e1);
+        (void)hipEventRecord(ev.e1, st);
+        hipError_t e = hipEventSynchronize(ev.e1);
         float ms = 0.f;
-        if (e == hipSuccess) (void)hipEventElapsedTime(&ms, e0, e1);
-        (void)hipEventDestroy(e0);
-        (void)hipEventDestroy(e1);
+        if (e == hipSuccess) (void)hipEventElapsedTime(&ms, ev.e0, ev.e1);
         if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
         *kernel_ms = ms;
     }
@@ -1092,6 +1104,15 @@ int bb_export(bb_sim *s, int32_t export_id, void **ptr, int32_t *dtype, int32_t 
 int64_t bb_num_worlds(const bb_sim *s) { return s ? s->cfg.num_worlds : 0; }
 int32_t bb_num_agents(const bb_sim *s) { return s ? s->n : 0; }
 int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
+
+// Diagnostic (not in the public header): k_rollout_split on (1), off (0) or
+// by grid size (-1) for the rollouts that follow (bit-parity tests of both).
+int bb_diag_force_rollout_split(int32_t v)
+{
+    if (v < -1 || v > 1) return fail(BB_ERR_INVALID_ARG, "bb_diag_force_rollout_split: -1, 0 or 1");
+    bb::force_rollout_split = v;
+    return BB_OK;
+}
 
 // Diagnostic (not in the public header): average ms of `iters` back-to-back
 // launches of a k_step variant (bb::StepMode) or, for mode 100, of a

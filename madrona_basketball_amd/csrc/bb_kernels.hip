@@ -522,33 +522,6 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
 }
 
 // One lane per agent: lane = (w - w0) * N + k.
-// k_step's copy of the erf Taylor table in LDS (BB_STEP_ERF_LDS, off): the
-// table's loads issued ahead of the state's, its LDS writes before the
-// systems.  Measured slower at every size (profiles/r03/i_erf_lds_ab.txt:
-// 8 192 worlds 11.65 -> 12.33 us, 65 536 21.9 -> 23.3, 262 144 74.6 -> 78.1):
-// the copy lengthens the load phase (0.96 -> 1.74 us at 8 192) while the
-// coefficient reads it removes are L2 hits off the critical path.
-#ifndef BB_STEP_ERF_LDS
-#define BB_STEP_ERF_LDS 0
-#endif
-constexpr int ERF_PER_LANE = (ERF_WORDS + WAVE - 1) / WAVE;
-__device__ __forceinline__ void erf_table_fetch(double (&e)[ERF_PER_LANE], int lane)
-{
-#pragma unroll
-    for (int j = 0; j < ERF_PER_LANE; j++) {
-        const int i = j * WAVE + lane;
-        e[j] = i < ERF_WORDS ? (&bbm::ERF_TAYLOR[0][0])[i] : 0.0;
-    }
-}
-__device__ __forceinline__ void erf_table_put(double *tab, const double (&e)[ERF_PER_LANE], int lane)
-{
-#pragma unroll
-    for (int j = 0; j < ERF_PER_LANE; j++) {
-        const int i = j * WAVE + lane;
-        if (i < ERF_WORDS) tab[i] = e[j];
-    }
-}
-
 template <int N, int MODE, bool LINES>
 __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 {
@@ -564,9 +537,6 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;  // the world with this lane's agent in slot 0
     trace_point<MODE>(p, 0);
-    double erf_words[ERF_PER_LANE];
-    __shared__ double erf_tab[BB_STEP_ERF_LDS ? ERF_WORDS : 1];
-    if constexpr (BB_STEP_ERF_LDS) erf_table_fetch(erf_words, lane);
     // The event-only words as loaded (store only on change, see Orig) wait
     // in the observation tile, which is free until the observation pass:
     // registers stay with the systems.
@@ -581,11 +551,6 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
             x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
             park_words(tile, lane, x);
         }
-    }
-    if constexpr (BB_STEP_ERF_LDS) {
-        erf_table_put(erf_tab, erf_words, lane);
-        wave_sync();
-        c.erf_tab = erf_tab;
     }
     if (active) {
         if constexpr (MODE == MODE_SKIP) step_world_pre_obs(s, c, ag, p.diag_skip, p.diag_dup);
@@ -615,40 +580,10 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
     trace_point<MODE>(p, 9);
 }
 
-// ------------------------------------------------------------------ wide step
-// Small world counts (C2, the reference's 8 192-world training batch: 256
-// waves of k_step = one per CU, 3 of every 4 SIMDs idle) leave k_step's time
-// to one wave's dependent chain.  k_step_wide gives each 32-world group a
-// workgroup of WIDE_WAVES waves on different SIMDs; all load the same worlds
-// and run the shared part of the chain (every system whose result another
-// system reads) redundantly -- free in latency, on otherwise idle SIMDs --
-// and split what only the outputs need:
-//   PCT    systems 1-8 only: the shot percentage (erf / atan, the longest
-//          per-agent tail) runs beside the others' systems 9-16 and reaches
-//          them through LDS (nothing in systems 9-17 reads it; a reset
-//          zeroes it, which the others see as their own reset);
-//   DEF    hardCodeDefense, then the Action and Attributes columns;
-//   STORE  reward, then every other state column (and the event-only words);
-//   OBS p  pass p of the observation rows (PhasedTile windows).
-// Every wave stores or emits a disjoint set of words, bit-identical to
-// k_step's (the same system code runs on the same inputs).
-constexpr int WIDE_DEF = 0, WIDE_PCT = 1, WIDE_STORE = 2, WIDE_OBS0 = 3;
-template <int N>
-struct Wide {
-    using T = StepTile<N, false>;
-    static constexpr int OBS_WAVES = T::PH;
-    static constexpr int WAVES = WIDE_OBS0 + OBS_WAVES;
-    static constexpr int TILES = 1 + OBS_WAVES;  // STORE's parked words, one tile per OBS wave
-    static constexpr int FLOATS = TILES * T::FLOATS + 2 * ERF_WORDS + WAVE;
-};
-#ifndef BB_WIDE_MAX_WAVES
-#define BB_WIDE_MAX_WAVES 0  // k_step_wide while k_step would have at most this many waves (0: never; A/B in DESIGN.md)
-#endif
-constexpr uint32_t SHOT_PCT_UNSET = 0x7FC0BEEFu;  // a NaN the step never computes
-
-
-template <int N, int PHASE, class T = typename Wide<N>::T>
-__device__ __forceinline__ void wide_obs_pass(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,
+// Pass PHASE of the observation rows of a wave that only writes rows (the
+// observation wave of k_rollout_split): its own tile, wave-local ordering.
+template <int N, int PHASE, class T = StepTile<N, false>>
+__device__ __forceinline__ void obs_pass_wave(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,
                                               int64_t w0, int64_t w, bool active, float *tile, float *obs)
 {
     SharedObs<N> sh;
@@ -661,214 +596,6 @@ __device__ __forceinline__ void wide_obs_pass(const World<N> &v, const Ctx &c, i
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
     constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
     flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, w0 * N, __ballot(fast), lane);
-}
-
-template <int N, int OP = 0>
-__device__ __forceinline__ void wide_obs_dispatch(int op, const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
-                                                  int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
-{
-    if constexpr (OP < Wide<N>::OBS_WAVES) {
-        if (op == OP) wide_obs_pass<N, OP>(v, c, ib, share, k, lane, w0, w, active, tile, obs);
-        else wide_obs_dispatch<N, OP + 1>(op, v, c, ib, share, k, lane, w0, w, active, tile, obs);
-    }
-}
-
-// MODE_TRACE: lane 0 of each wave records the clock at 0 start, 1 state
-// loaded, 2 after the first barrier, 3 systems done, 4 after the second
-// barrier, 9 end, into diag_ts[(workgroup * WAVES + wave) * TRACE_POINTS].
-template <int N, int MODE>
-__device__ __forceinline__ void wide_trace(const Params &p, int wave, int point)
-{
-    if constexpr (MODE == MODE_TRACE) {
-        if (point == 1) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint64_t t = wall_clock64();
-        if (threadIdx.x % WAVE == 0)
-            p.diag_ts[((int64_t)blockIdx.x * Wide<N>::WAVES + wave) * TRACE_POINTS + point] = t;
-    }
-}
-
-template <int N, int MODE = MODE_FULL>
-__device__ __forceinline__ void step_agent_lanes_wide(const Params &p, float *lds)
-{
-    using T = typename Wide<N>::T;
-    const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-    const int lane = (int)threadIdx.x % WAVE;
-    const int k = lane % N;
-    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
-    const int64_t w = w0 + lane / N;
-    const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
-    const LaneAgents<N, MODE_FULL> ag{k, &p};
-    // LDS: [STORE parked words | OBS tiles][erf table (PCT)][shot percentages]
-    float *tile = lds + (wave >= WIDE_STORE ? (wave - WIDE_STORE) * T::FLOATS : 0);
-    double *erf_tab = (double *)(lds + Wide<N>::TILES * T::FLOATS);
-    float *pct = lds + Wide<N>::TILES * T::FLOATS + 2 * ERF_WORDS;
-
-    World<N> s;
-    // memory side effects of the systems (Stats, Team in score / reset) from
-    // one wave only
-    Ctx c = make_ctx(p, w, k == 0 && wave == WIDE_STORE);
-    wide_trace<N, MODE>(p, wave, 0);
-    if (wave == WIDE_PCT) {
-        // the erf table into LDS (its loads issued before the state's)
-        double e[(ERF_WORDS + WAVE - 1) / WAVE];
-#pragma unroll
-        for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
-            const int i = j * WAVE + lane;
-            e[j] = i < ERF_WORDS ? (&bbm::ERF_TAYLOR[0][0])[i] : 0.0;
-        }
-        if (active) load_world(s, p, w);
-#pragma unroll
-        for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
-            const int i = j * WAVE + lane;
-            if (i < ERF_WORDS) erf_tab[i] = e[j];
-        }
-        wave_sync();
-        c.erf_tab = erf_tab;
-    } else if (active) {
-        load_world(s, p, w);
-    }
-    if (wave == WIDE_STORE && active) {
-        Orig<N> o;
-        capture(o, s);
-        LaneOrig x;
-        x.world = world_orig(o);
-        x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
-        park_words(tile, lane, x);
-    }
-    wide_trace<N, MODE>(p, wave, 1);
-    // every wave has loaded the columns before any wave writes one (the
-    // systems' own side effects: Stats, Team)
-    __syncthreads();
-    wide_trace<N, MODE>(p, wave, 2);
-    if (active) {
-        constexpr uint32_t LATE = (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14)
-                                  | (1u << 15) | (1u << 16) | (1u << 17);
-        uint32_t skip;
-        if (wave == WIDE_PCT) {
-            skip = LATE;  // systems 1-8
-        } else {
-            skip = (1u << 8) | (1u << 17);  // all but the shot percentage and the defence
-#pragma unroll
-            for (int i = 0; i < N; i++) s.attr[i][8] = bitsf(SHOT_PCT_UNSET);
-        }
-        step_world_pre_obs(s, c, ag, skip, 0u);
-        if (wave == WIDE_PCT) pct[lane] = pick_by<N>(k, [&](int j) { return s.attr[j][8]; });
-    }
-    wide_trace<N, MODE>(p, wave, 3);
-    __syncthreads();  // the shot percentages are in LDS
-    wide_trace<N, MODE>(p, wave, 4);
-    if (wave == WIDE_PCT) {  // (no workgroup barrier follows)
-        wide_trace<N, MODE>(p, wave, 9);
-        return;
-    }
-    if (active) {
-        // systems 9-17 left attribute 8 alone unless a reset zeroed it
-#pragma unroll
-        for (int i = 0; i < N; i++)
-            if (fbits(s.attr[i][8]) == SHOT_PCT_UNSET) s.attr[i][8] = pct[lane - k + i];
-    }
-    World<N> v;  // the world with this lane's agent in slot 0
-    if (wave == WIDE_DEF) {
-        if (active) {
-            sys_defense(s, c, ag);
-            agent_view(s, v, k);
-            store_world_agent<N, -1, STORE_ACT_ATTR>(v, p, w * N + k, 0);
-        }
-    } else if (wave == WIDE_STORE) {
-        if (active) {
-            agent_view(s, v, k);
-            sys_reward_agent(v, 0, AGENT0_ID + k);
-            const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
-            store_world_agent<N, -1, STORE_REST>(v, p, w * N + k, 0, &x.agent);
-            if (k == 0) {
-                Orig<N> o;
-                set_world_orig(o, x.world);
-                store_world_shared(s, p, w, &o);
-            }
-        }
-    } else {
-        if (active) agent_view(s, v, k);
-        const int32_t ib = active ? inbounder_id(s) : -1;
-        const bool share = active && obs_sharable(s);
-        wide_obs_dispatch<N>(wave - WIDE_OBS0, v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
-    }
-    wide_trace<N, MODE>(p, wave, 9);
-}
-
-template <int N, int MODE = MODE_FULL>
-__global__ __launch_bounds__(WAVE * Wide<N>::WAVES, 1) void k_step_wide(const Params p)
-{
-    if constexpr (N == 2 && BB_AGENT_LANES && !Lanes<N>::SHARED) {
-        __shared__ float4 lds4[(Wide<N>::FLOATS + 3) / 4];
-        step_agent_lanes_wide<N, MODE>(p, (float *)lds4);
-    }
-}
-
-// Timing experiment (diagnostic build, BB_STEP_BLOCKS > 1): each wave steps
-// B world blocks in turn, the next block's state loads issued ahead of this
-// block's systems and retired before its stores (the k_rollout discipline),
-// so a block's row stores drain under the next block's systems.  Same
-// results as k_step with one block per wave (every world is stepped once,
-// by the same code).
-#ifndef BB_STEP_BLOCKS
-#define BB_STEP_BLOCKS 1
-#endif
-template <int N, bool LINES, int B>
-__device__ __forceinline__ void step_agent_lanes_pipelined(const Params &p, float *tile)
-{
-    using T = StepTile<N, LINES>;
-    const int lane = threadIdx.x;
-    const int k = lane % N;
-    const int64_t nblk = (p.num_worlds + WAVE / N - 1) / (WAVE / N);
-    const int64_t stride = (int64_t)gridDim.x * (WAVE / N);
-    World<N> nxt;
-    {
-        const int64_t w = (int64_t)blockIdx.x * (WAVE / N) + lane / N;
-        if (w < p.num_worlds) load_world(nxt, p, w);
-    }
-    for (int b = 0; b < B; b++) {
-        const int64_t blk = (int64_t)blockIdx.x + (int64_t)b * gridDim.x;
-        if (blk >= nblk) break;  // uniform over the wave
-        const int64_t w0 = blk * (WAVE / N);
-        const int64_t w = w0 + lane / N;
-        const bool active = w < p.num_worlds;
-        const int64_t wn = w + stride;
-        const bool next_ok = b + 1 < B && wn < p.num_worlds;
-        const LaneAgents<N, MODE_FULL> ag{k, &p};
-        World<N> s = nxt;
-        World<N> v;
-        Ctx c = make_ctx(p, w, k == 0);
-        if (active) {
-            {
-                Orig<N> o;
-                capture(o, s);
-                LaneOrig x;
-                x.world = world_orig(o);
-                x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
-                park_words(tile, lane, x);
-            }
-            if (next_ok) load_world(nxt, p, wn);
-            step_world_pre_obs(s, c, ag);
-        }
-        // the prefetch retired here: what it waits for besides it are the
-        // previous block's stores, drained during these systems
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-        if (active) {
-            agent_view(s, v, k);
-            sys_reward_agent(v, 0, AGENT0_ID + k);
-            const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
-            store_world_agent(v, p, w * N + k, 0, &x.agent);
-            if (k == 0) {
-                Orig<N> o;
-                set_world_orig(o, x.world);
-                store_world_shared(s, p, w, &o);
-            }
-        }
-        const int32_t ib = active ? inbounder_id(s) : -1;
-        const bool share = active && obs_sharable(s);
-        agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
-        __syncthreads();  // the tile's rows (and parked words) are rewritten by the next block
-    }
 }
 
 // ------------------------------------------------------------------ rollout
@@ -1122,10 +849,10 @@ __device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArg
         const bool share = u[SplitView<N>::WORDS - 1] != 0u;
         const Ctx c = make_ctx(p, w, k == 0);
         float *obs = r.obs + (int64_t)t * r.obs_step;
-        wide_obs_pass<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+        obs_pass_wave<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
         wave_sync();  // the tile is rewritten by the next pass
         if constexpr (T::PH > 1) {
-            wide_obs_pass<N, 1, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+            obs_pass_wave<N, 1, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
             wave_sync();
         }
         static_assert(T::PH <= 2, "two row passes");
@@ -1141,84 +868,6 @@ __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, c
         __shared__ uint32_t park[6 * WAVE];
         if (__builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE) == 0) split_sim_wave<N>(p, r, view, park);
         else split_obs_wave<N>(p, r, view, (float *)tile4);
-    }
-}
-
-// ------------------------------------------------------------------ split step
-// One step over two waves per 32 worlds (small grids, N = 2): the sim wave S
-// loads the worlds, runs systems 1-17 and hands each lane's view of its world
-// to the observation wave O through LDS (SplitView, as k_rollout_split); O
-// writes the observation rows while S runs the reward and stores the state
-// columns, so the step costs load + systems + max(reward + stores, rows)
-// instead of their sum.  Same system, reward, store and row code on the same
-// inputs as k_step: bit-identical.
-template <int N>
-__global__ __launch_bounds__(2 * WAVE, 1) void k_step_split(const Params p)
-{
-    if constexpr (FusedRollout<N>::value) {
-        using T = StepTile<N, false>;
-        __shared__ SplitView<N> view;
-        __shared__ float4 tile4[T::FLOATS / 4];
-        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-        const int lane = (int)threadIdx.x % WAVE;
-        const int k = lane % N;
-        const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
-        const int64_t w = w0 + lane / N;
-        const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
-        if (wave == 0) {
-            const LaneAgents<N, MODE_FULL> ag{k, &p};
-            Ctx c = make_ctx(p, w, k == 0);
-            World<N> s, v;
-            LaneOrig x;
-            int32_t ib = -1;
-            bool share = false;
-            if (active) {
-                load_world(s, p, w);
-                Orig<N> o;
-                capture(o, s);
-                x.world = world_orig(o);
-                x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
-                step_world_pre_obs(s, c, ag);
-                agent_view(s, v, k);
-                ib = inbounder_id(s);
-                share = obs_sharable(s);
-                uint32_t u[SplitView<N>::WORDS];
-                __builtin_memcpy(u, &v, sizeof(World<N>));
-                u[SplitView<N>::WORDS - 2] = (uint32_t)ib;
-                u[SplitView<N>::WORDS - 1] = share ? 1u : 0u;
-#pragma unroll
-                for (int i = 0; i < SplitView<N>::WORDS; i++) view.w[i][lane] = u[i];
-            }
-            lds_barrier();  // the views are in LDS
-            if (active) {
-                sys_reward_agent(v, 0, AGENT0_ID + k);
-                store_world_agent<N, BB_COL_AUX>(v, p, w * N + k, 0, &x.agent);
-                if (k == 0) {
-                    Orig<N> o;
-                    set_world_orig(o, x.world);
-                    store_world_shared<N, BB_COL_AUX>(s, p, w, &o);
-                }
-            }
-        } else {
-            lds_barrier();  // the views are in LDS
-            World<N> v;
-            int32_t ib = -1;
-            bool share = false;
-            if (active) {
-                uint32_t u[SplitView<N>::WORDS];
-#pragma unroll
-                for (int i = 0; i < SplitView<N>::WORDS; i++) u[i] = view.w[i][lane];
-                __builtin_memcpy(&v, u, sizeof(World<N>));
-                ib = (int32_t)u[SplitView<N>::WORDS - 2];
-                share = u[SplitView<N>::WORDS - 1] != 0u;
-            }
-            const Ctx c = make_ctx(p, w, k == 0);
-            float *tile = (float *)tile4;
-            wide_obs_pass<N, 0, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
-            wave_sync();  // the tile is rewritten by the next pass
-            if constexpr (T::PH > 1) wide_obs_pass<N, 1, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
-            static_assert(T::PH <= 2, "two row passes");
-        }
     }
 }
 
@@ -1383,9 +1032,9 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             }
         }
         if (t + 1 == r.steps) {  // the sim's observation tensor: every row of the last step
-            wide_obs_pass<N, 0>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
+            obs_pass_wave<N, 0>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
             wave_sync();
-            wide_obs_pass<N, 1>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
+            obs_pass_wave<N, 1>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
         }
         wave_sync();
         ppo_trace(r, t, 2);
@@ -1829,77 +1478,11 @@ __device__ __forceinline__ void emit_pieces_rows(const SharedLds<N> &sm, uint64_
         emit_slot_batches<N, AUX, S0, S1, NP, RB, 0>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
 
-// Row groups as one stretch of pieces (BB_OBS_FLAT): a group of G
-// consecutive rows of one world is G * QR consecutive 16-byte pieces, written
-// by ceil(G * QR / 64) whole-wave store instructions -- instruction i, lane L:
-// piece 64 i + L of the group -- instead of ceil(QR / 64) per row (N = 4:
-// 46 of 64 lanes per row; N = 10: 64 + 42).  A lane's pieces are then at
-// different row positions (row 64 i + L div QR of the group), decoded once
-// per instruction slot i and per group of the world (the observer is
-// g G + that row), before the loop.
-#ifndef BB_OBS_FLAT
-#define BB_OBS_FLAT 0  // measured slower (profiles/r03/ar_*): N = 4 63.9-65.5 vs 63.5-64.4 us, N = 10 293-294 vs 285-288
-#endif
-template <int N>
-struct FlatGroups {
-    static constexpr int QR = ObsSrc<N>::QR;
-    static constexpr int G = N <= 4 ? N : N / 2;  // rows per group
-    static constexpr int NG = N / G;               // groups per world
-    static constexpr int GQ = G * QR;              // pieces per group
-    static constexpr int INS = (GQ + WAVE - 1) / WAVE;
-    static_assert(N % G == 0, "whole groups per world");
-};
-template <int N, int AUX, int S0, int S1>
-__device__ __forceinline__ void emit_pieces_flat(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
-                                                 int64_t row0, int lane)
-{
-    using F = FlatGroups<N>;
-    constexpr int QR = F::QR, G = F::G, NG = F::NG, GQ = F::GQ, INS = F::INS;
-    int src[NG][INS][4], dtm[INS][4], rg[INS];
-#pragma unroll
-    for (int i = 0; i < INS; i++) {
-        const int f = i * WAVE + lane;
-        const bool ok = f < GQ;
-        const int r = ok ? f / QR : 0, q = ok ? f - r * QR : 0;
-        rg[i] = ok ? r : 63;  // 63: no row (the row bits above G are cleared below)
-        const uint4 cd = sm.code[q];
-        const uint32_t code[4] = {cd.x, cd.y, cd.z, cd.w};
-#pragma unroll
-        for (int c = 0; c < 4; c++) {
-#pragma unroll
-            for (int g = 0; g < NG; g++) src[g][i][c] = esw(piece_src<N>(code[c], g * G + r, 0));
-            dtm[i][c] = esw(piece_src<N>(code[c], 0, 1)) - esw(piece_src<N>(code[c], 0, 0));  // context entries only
-        }
-    }
-    char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
-    constexpr uint64_t GMASK = (1ull << G) - 1;
-    for (int slot = S0; slot < S1; slot++) {
-        const float *e = sm.e[slot - S0];
-#pragma unroll
-        for (int g = 0; g < NG; g++) {
-            const int r0 = slot * N + g * G;
-            const uint64_t gm = (rows >> r0) & GMASK, gt = (teams >> r0) & GMASK;
-            if (!gm) continue;  // wave-uniform
-            vf4 v[INS];
-#pragma unroll
-            for (int i = 0; i < INS; i++) {
-                const int tm = -(int)((gt >> rg[i]) & 1ull);  // team 1: all ones
-                v[i] = vf4{e[src[g][i][0] + (dtm[i][0] & tm)], e[src[g][i][1] + (dtm[i][1] & tm)],
-                           e[src[g][i][2] + (dtm[i][2] & tm)], e[src[g][i][3] + (dtm[i][3] & tm)]};
-            }
-            const uint32_t off0 = (uint32_t)r0 * QR * 16u;
-#pragma unroll
-            for (int i = 0; i < INS; i++)
-                if ((gm >> rg[i]) & 1ull) row_store<AUX>(base, off0 + (uint32_t)(i * WAVE + lane) * 16u, v[i]);
-        }
-    }
-}
 template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
 __device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
                                             int64_t row0, int lane)
 {
-    if constexpr (BB_OBS_FLAT) emit_pieces_flat<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
-    else emit_pieces_rows<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
+    emit_pieces_rows<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
 }
 
 // The source table written and emitted part by part (BB_OBS_PARTS): the
@@ -2188,8 +1771,6 @@ __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
             for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
         }
         step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm);
-    } else if constexpr (Lanes<N>::LPW == N && MODE == MODE_FULL && BB_STEP_BLOCKS > 1) {
-        step_agent_lanes_pipelined<N, LINES, BB_STEP_BLOCKS>(p, (float *)tile4);
     } else if constexpr (Lanes<N>::LPW == N) {
         step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);
     } else {
@@ -2230,46 +1811,6 @@ bool step_lines(int64_t num_worlds)
     return Lanes<N>::LPW == N && num_worlds * per_world > LINES_MIN_BYTES;
 }
 
-// k_step_wide (N = 2) while k_step would run at most BB_WIDE_MAX_WAVES waves
-// (MADRONA_BB_WIDE_MAX_WAVES overrides it for A/B timing; 0 disables).
-inline int64_t wide_max_waves()
-{
-    static const int64_t v = [] {
-        const char *e = getenv("MADRONA_BB_WIDE_MAX_WAVES");
-        return (int64_t)(e && *e ? atoll(e) : BB_WIDE_MAX_WAVES);
-    }();
-    return v;
-}
-template <int N>
-bool step_wide(int64_t num_worlds)
-{
-    if constexpr (N == 2 && BB_AGENT_LANES && !Lanes<N>::SHARED && BB_STEP_BLOCKS == 1) {
-        return (num_worlds + Lanes<N>::WPB - 1) / Lanes<N>::WPB <= wide_max_waves();
-    } else {
-        return false;
-    }
-}
-
-// Compute units of the current device (256 on MI355X).
-static unsigned device_cus();
-
-// k_step_split (N = 2) while the step has at most this many worlds;
-// MADRONA_BB_STEP_SPLIT_MAX_WORLDS overrides it (0: never).
-#ifndef BB_STEP_SPLIT_MAX_WORLDS
-#define BB_STEP_SPLIT_MAX_WORLDS 0
-#endif
-template <int N>
-bool step_split(int64_t num_worlds)
-{
-    if constexpr (N == 2 && FusedRollout<N>::value && BB_STEP_BLOCKS == 1) {
-        const char *e = getenv("MADRONA_BB_STEP_SPLIT_MAX_WORLDS");  // read per launch (tests run both)
-        const int64_t mx = e && *e ? atoll(e) : BB_STEP_SPLIT_MAX_WORLDS;
-        return num_worlds <= mx;
-    } else {
-        return false;
-    }
-}
-
 // Compute units of the current device (256 on MI355X).
 static unsigned device_cus()
 {
@@ -2287,30 +1828,18 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 {
     constexpr int WPB = Lanes<N>::WPB;
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-    // BB_STEP_BLOCKS world blocks per wave (the pipelined timing experiment)
-    constexpr int FB = (Lanes<N>::LPW == N && !Lanes<N>::SHARED) ? BB_STEP_BLOCKS : 1;
-    const dim3 grid_full((grid.x + FB - 1) / FB);
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
     switch (mode) {
     case MODE_FULL:
-        if (step_split<N>(p.num_worlds))
-            hipExtLaunchKernelGGL(k_step_split<N>, grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p);
-        else if (step_wide<N>(p.num_worlds))
-            hipExtLaunchKernelGGL(k_step_wide<N>, grid, dim3(WAVE * Wide<N>::WAVES), 0, s, ev0, ev1, 0, p);
-        else if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid_full, block, 0, s, ev0, ev1, 0, p);
-        else hipExtLaunchKernelGGL(k_step<N, MODE_FULL>, grid_full, block, 0, s, ev0, ev1, 0, p);
+        if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid, block, 0, s, ev0, ev1, 0, p);
+        else hipExtLaunchKernelGGL(k_step<N, MODE_FULL>, grid, block, 0, s, ev0, ev1, 0, p);
         break;
     case MODE_IO: BB_LAUNCH(MODE_IO); break;
     case MODE_IO_OBS: BB_LAUNCH(MODE_IO_OBS); break;
     case MODE_DIRECT_OBS: BB_LAUNCH(MODE_DIRECT_OBS); break;
     case MODE_NO_OBS: BB_LAUNCH(MODE_NO_OBS); break;
     case MODE_SKIP: BB_LAUNCH(MODE_SKIP); break;
-    case MODE_TRACE:
-        if (step_wide<N>(p.num_worlds))
-            hipExtLaunchKernelGGL(k_step_wide<N, MODE_TRACE>, grid, dim3(WAVE * Wide<N>::WAVES), 0, s, ev0, ev1, 0, p);
-        else
-            BB_LAUNCH(MODE_TRACE);
-        break;
+    case MODE_TRACE: BB_LAUNCH(MODE_TRACE); break;
     default: return hipErrorInvalidValue;
     }
 #undef BB_LAUNCH
@@ -2318,24 +1847,28 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 }
 
 // The whole-register-file rollout while the grid fits one wave per SIMD (every
-// CU of the device, 4 SIMDs each); env MADRONA_BB_ROLLOUT_MINW=1/2 forces it.
+// CU of the device, 4 SIMDs each); env MADRONA_BB_ROLLOUT_MINW=1/2 forces it
+// (read once per process).
 static bool rollout_minw1(unsigned waves)
 {
-    const char *e = getenv("MADRONA_BB_ROLLOUT_MINW");
-    const int forced = e && *e ? atoi(e) : 0;
+    static const int forced = [] {
+        const char *e = getenv("MADRONA_BB_ROLLOUT_MINW");
+        return e && *e ? atoi(e) : 0;
+    }();
     if (forced) return forced == 1;
     return waves <= 4u * device_cus();
 }
 
-// k_rollout_split while its workgroups (2 waves) fit one wave per SIMD:
-// at most 2 per CU.  MADRONA_BB_ROLLOUT_SPLIT=0/1 forces it off / on (A/B).
+// k_rollout_split while its workgroups (2 waves) fit one wave per SIMD: at
+// most 2 per CU.  force_rollout_split (bb_common.hip: MADRONA_BB_ROLLOUT_SPLIT
+// at load, bb_diag_force_rollout_split at run time) forces it off / on (A/B,
+// tests).
 #ifndef BB_ROLLOUT_SPLIT
 #define BB_ROLLOUT_SPLIT 1
 #endif
 static bool rollout_split(unsigned groups)
 {
-    const char *e = getenv("MADRONA_BB_ROLLOUT_SPLIT");  // read per launch: the tests run both kernels
-    const int forced = e && *e ? atoi(e) : -1;
+    const int forced = force_rollout_split;
     if (forced >= 0) return forced != 0;
     return BB_ROLLOUT_SPLIT != 0 && groups <= 2u * device_cus();
 }
@@ -2384,8 +1917,7 @@ template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRo
 template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value; }
 template <> int step_grid<BB_N>(int64_t num_worlds)
 {
-    const int g = (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB);
-    return step_wide<BB_N>(num_worlds) ? g * Wide<BB_N>::WAVES : g;  // waves of the MODE_FULL launch
+    return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB);  // waves of the MODE_FULL launch
 }
 
 }  // namespace bb

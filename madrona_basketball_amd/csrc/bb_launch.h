@@ -55,6 +55,10 @@ struct RecordArgs {
 int32_t record_words(int n);
 RecordArgs record_args(const Params &p, int n);
 
+// k_rollout_split choice: -1 by grid size, 0 never, 1 always (diagnostics and
+// tests; bb_common.hip, bb_diag_force_rollout_split).
+extern int force_rollout_split;
+
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
 template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)

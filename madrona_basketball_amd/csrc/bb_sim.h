@@ -185,10 +185,11 @@ BB_HD float uni(float x)
 #endif
 }
 BB_HD F3 uni(F3 a) { return f3(uni(a.x), uni(a.y), uni(a.z)); }
-// A kernel-argument value kept in a scalar register and opaque to the
-// optimiser (so that a chain of selects over a table is not folded back into
-// a per-lane indexed load), without uni()'s readfirstlane, which is
-// convergent and keeps every branch around it from being if-converted.
+// A kernel-argument value used as it is: uni() without the readfirstlane.
+// The identity itself hides nothing from the optimiser; what changes the
+// generated code is the missing readfirstlane, which is convergent and keeps
+// every branch around it from being if-converted (the values are uniform
+// kernel arguments, held in scalar registers anyway).
 BB_HD float sconst(float x)
 {
     return x;

@@ -199,7 +199,7 @@ class FusedPolicy:
         buffer stores of ppo.py:129-134 and next_value = evaluate(last obs).
         Bit for bit n x (act(); [opponent.act()]; sim.step()) with the same reads.
         Any entry of `buffers` may be None (not recorded).  On gfx950 (2 agents,
-        no opponent, up to 8 192 worlds) one fused launch runs every step;
+        no opponent, up to 16 384 worlds) one fused launch runs every step;
         per_step=True forces a policy launch + a step launch per step.  Returns
         the elapsed device ms when time_kernels."""
         W = sim.num_worlds

@@ -140,22 +140,29 @@ def test_gpu_fused_rollout_equals_per_step_and_host(native_lib, flags):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W", [8190, 16384])
-def test_gpu_split_rollout_equals_single_wave_rollout(native_lib, monkeypatch, W):
+def test_gpu_split_rollout_equals_single_wave_rollout(native_lib, W):
     """k_rollout_split (a sim wave + an observation wave per 32 worlds, taken
-    up to 2 workgroups per CU) == k_rollout (one wave, MADRONA_BB_ROLLOUT_SPLIT=0)
-    bit for bit: every recorded step, the written-back actions, the state."""
+    up to 2 workgroups per CU) == k_rollout (one wave; forced by the
+    diagnostic bb_diag_force_rollout_split) bit for bit: every recorded step,
+    the written-back actions, the state."""
     _gpu()
+    import ctypes
+    force = native_lib.bb_diag_force_rollout_split
+    force.restype, force.argtypes = ctypes.c_int, [ctypes.c_int32]
     K = 64
     outs = []
-    for split in ("1", "0"):
-        monkeypatch.setenv("MADRONA_BB_ROLLOUT_SPLIT", split)
-        sim = make_sim(ExecMode.CUDA, W, per_world_rng=True, tag_mask=False)
-        acts = sim.stage_random_actions(K, action_seed=5, step0=0)
-        buf = sim.rollout_buffers(K)
-        sim.rollout(acts, buf["obs"], buf["reward"], buf["done"])
-        sim.rollout(acts[: K // 2].clone())  # unrecorded: every step's rows into the sim's own tensor
-        torch.cuda.synchronize()
-        outs.append((sim, acts, buf))
+    try:
+        for split in (1, 0):
+            assert force(split) == 0
+            sim = make_sim(ExecMode.CUDA, W, per_world_rng=True, tag_mask=False)
+            acts = sim.stage_random_actions(K, action_seed=5, step0=0)
+            buf = sim.rollout_buffers(K)
+            sim.rollout(acts, buf["obs"], buf["reward"], buf["done"])
+            sim.rollout(acts[: K // 2].clone())  # unrecorded: every step's rows into the sim's own tensor
+            torch.cuda.synchronize()
+            outs.append((sim, acts, buf))
+    finally:
+        force(-1)
     (a, acts_a, buf_a), (b, acts_b, buf_b) = outs
     assert_same(acts_a, acts_b, "actions")
     for key in ("obs", "reward", "done"):
