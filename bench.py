@@ -327,16 +327,18 @@ def main():
     # "5v5" extensions (65 536 x 4 / x 10); each events-timed over
     # >= EVENT_MIN_LAUNCHES launches like the headline kernel
     extra = {}
-    if (on_gpu and not args.no_configs and not args.policy and not K and world_size == 1
+    if (on_gpu and not args.no_configs and not args.policy and not K
             and W == 65536 and args.agents == 2):
         L0 = _lib.load()
 
         def config_line(W2, n2, K2=0, launches=EVENT_MIN_LAUNCHES):
+            """W2 worlds per rank (world_offset = rank * W2); wall time and
+            kernel time are the maxima over ranks, value = all ranks' worlds."""
             steps2 = launches * (K2 or 1)
             sim2 = mba.SimpleGridworldSimulator(
                 discrete_x=32, discrete_y=17, start_x=31.515 / 2.0, start_y=16.764000000000003 / 2.0,
                 max_episode_length=39600, exec_mode=mba.ExecMode.CUDA, num_worlds=W2, gpu_id=dev.index,
-                num_agents=n2, per_world_rng=True)
+                num_agents=n2, per_world_rng=True, world_offset=rank * W2)
             sim2.step_n(20, random_actions=True, action_seed=args.seed, step0=0)
             bufs2 = sim2.rollout_buffers(K2) if K2 else None
 
@@ -349,21 +351,25 @@ def main():
                                        time_kernels=timed) or 0.0
                 return ms
             acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20)
-            sync()
+            barrier()
             t0 = time.perf_counter()
             go(acts2, False)
             sync()
             wall2 = time.perf_counter() - t0
+            barrier()
+            wall2 = max_over_ranks(wall2)
             acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20 + steps2)
-            sync()
-            k2 = go(acts2, True) / 1e3 / launches
+            barrier()
+            k2 = max_over_ranks(go(acts2, True) / 1e3 / launches)
+            barrier()
             fused2 = bool(L0.bb_rollout_fused(n2)) and K2 > 0
             if fused2:
                 b2 = W2 * (K2 * L0.bb_rollout_bytes_per_world_step(n2) + L0.bb_rollout_state_bytes_per_world(n2))
             else:
                 b2 = L0.bb_algorithmic_bytes_per_world(n2) * W2 * (K2 or 1)
             key = f"W{W2}_N{n2}" + (f"_R{K2}" if K2 else "")
-            line = {"worlds": W2, "agents": n2, "steps": steps2, "value": W2 * steps2 / wall2, "unit": "env-steps/s",
+            line = {"worlds": W2 * world_size, "worlds_per_gpu": W2, "n_gpus": world_size, "agents": n2,
+                    "steps": steps2, "value": W2 * world_size * steps2 / wall2, "unit": "env-steps/s",
                     "ms_per_step": wall2 * 1e3 / steps2,
                     "kernel": ("bb::k_rollout<%d>" if fused2 else "bb::k_step<%d>") % n2,
                     "launches_timed": launches, "kernel_avg_us": k2 * 1e6,
@@ -406,14 +412,19 @@ def main():
             torch.cuda.empty_cache()
             return line
 
-        extra["roofline_beyond_cache"] = config_line(262144, 2)
-        extra["config_c2_8192x2"] = config_line(8192, 2)
-        extra["config_c2_8192x2_rollout32"] = config_line(8192, 2, 32, launches=EVENT_MIN_LAUNCHES // 4)
-        extra["config_c4_shard_32768x2"] = config_line(32768, 2)
-        extra["config_2v2_65536x4"] = config_line(65536, 4)
-        extra["config_c5_65536x10"] = config_line(65536, 10)
-        extra["ppo_rollout32_8192x2"] = ppo_line(8192)
-        extra["ppo_rollout32_65536x2"] = ppo_line(65536)
+        if world_size == 1:
+            extra["roofline_beyond_cache"] = config_line(262144, 2)
+            extra["config_c2_8192x2"] = config_line(8192, 2)
+            extra["config_c2_8192x2_rollout32"] = config_line(8192, 2, 32, launches=EVENT_MIN_LAUNCHES // 4)
+            extra["config_c4_shard_32768x2"] = config_line(32768, 2)
+            extra["config_2v2_65536x4"] = config_line(65536, 4)
+            extra["config_c5_65536x10"] = config_line(65536, 10)
+            extra["ppo_rollout32_8192x2"] = ppo_line(8192)
+            extra["ppo_rollout32_65536x2"] = ppo_line(65536)
+        else:
+            # BASELINE configs[3] as stated: 32 768 worlds per GPU, all ranks
+            # stepping their shard together (262 144 worlds at 8 GPUs)
+            extra["config_c4_32768_per_gpu"] = config_line(32768, 2)
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed

@@ -13,7 +13,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liboracle_bb.so")
+# MADRONA_BB_ORACLE_LIB: a sanitizer build of the same source (tools/sanitize.sh)
+LIB_PATH = os.environ.get("MADRONA_BB_ORACLE_LIB") or os.path.join(HERE, "liboracle_bb.so")
 
 # Export ids (reference src/types.hpp:10-42) and build-internal state ids.
 EXPORTS = {
