@@ -104,11 +104,13 @@ def test_gpu_policy_rollout_equals_the_ppo_loop(native_lib, trainee, stochastic,
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("W,n,trainee,stochastic", [(8192, 32, 0, True), (1000, 20, 1, False), (64, 3, 0, True)])
+@pytest.mark.parametrize("W,n,trainee,stochastic", [(8192, 32, 0, True), (1000, 20, 1, False), (64, 3, 0, True),
+                                                    (16384, 16, 1, True), (12345, 8, 0, False)])
 def test_gpu_fused_policy_rollout_equals_per_step_launches(native_lib, W, n, trainee, stochastic):
     """The fused PPO rollout kernel (one launch, k_rollout_policy) == a policy
     launch + a step launch per step, every output and every column, bit for bit
-    (a partial last workgroup included: W = 1000, 64)."""
+    (a partial last workgroup included: W = 1000, 64, 12345; 16 384 = the fused
+    kernel's default bound, two workgroups per CU)."""
     assert torch.cuda.is_available()
     sims = [make_sim(ExecMode.CUDA, W, per_world_rng=True) for _ in range(2)]
     for s in sims:
@@ -121,6 +123,15 @@ def test_gpu_fused_policy_rollout_equals_per_step_launches(native_lib, W, n, tra
     assert_same(bufs[0], bufs[1])
     for name in sims[0]._views:
         assert torch.equal(sims[0]._views[name], sims[1]._views[name]), name
+
+
+@pytest.mark.gpu
+def test_gpu_policy_rollout_at_65536_worlds_equals_the_ppo_loop(native_lib):
+    """BASELINE configs[2]'s world count (the bench's ppo_rollout32_65536x2
+    line): the default rollout path at 65 536 worlds == FusedPolicy.act +
+    step per step, every output and every column."""
+    assert torch.cuda.is_available()
+    run_pair(ExecMode.CUDA, 65536, 8, 0, True, False, "cuda")
 
 
 @pytest.mark.gpu
