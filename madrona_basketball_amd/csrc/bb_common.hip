@@ -140,6 +140,79 @@ __global__ __launch_bounds__(256) void k_math_probe(int fn, const float *x, cons
     out[i] = r;
 }
 
+// Diagnostics (tests/test_gpu_math.py): bbm's short-path divide / square root
+// (bb_math.h) against the IEEE operations compiled by hipcc, on the device.
+// mode 0 sqrt_short, 1 rcp refined only, 2 rcp_short<1>, 3 div_short<1>,
+// 4 div_short<2>, 5 the bare v_sqrt_f32.  Modes 0-2 and 5 take the float bit
+// patterns start + i, i < count, skipping those outside the short path's
+// range; modes 3-4 take pseudo-random operand pairs (index i, seed) with
+// exponents in the short path's range.  Per workgroup: the mismatch count and
+// one mismatching input (a bits, b bits).
+__device__ __forceinline__ uint32_t probe_hash(uint32_t x)
+{
+    x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ float probe_operand(uint32_t h, uint32_t e_lo, uint32_t e_hi)
+{
+    const uint32_t e = e_lo + (uint32_t)(((uint64_t)(h >> 8) * (e_hi - e_lo + 1)) >> 24);
+    return __builtin_bit_cast(float, (h & 0x80000000u) | (e << 23) | (probe_hash(h) & 0x7fffffu));
+}
+__global__ __launch_bounds__(256) void k_divsqrt_probe(int mode, uint64_t start, uint64_t count, uint32_t seed,
+                                                       uint32_t *counts, uint32_t *ex)
+{
+    const uint64_t nth = (uint64_t)gridDim.x * 256;
+    uint32_t bad = 0, ea = 0, eb = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += nth) {
+        float a = 0.f, b = 0.f, got = 0.f, want = 0.f;
+        bool in = true;
+        if (mode == 3 || mode == 4) {
+            const uint32_t h = probe_hash((uint32_t)i ^ probe_hash(seed + (uint32_t)(i >> 32)));
+            a = probe_operand(h, 80u, 174u);
+            b = probe_operand(probe_hash(h ^ 0x9e3779b9u), 80u, 174u);
+            got = mode == 3 ? bbm::div_short<1>(a, b) : bbm::div_short<2>(a, b);
+            want = a / b;
+        } else {
+            b = __builtin_bit_cast(float, (uint32_t)(start + i));
+            if (mode == 0 || mode == 5) {
+                in = !(bbm::f2u(b) >> 31) && bbm::exp_in(b, mode == 0 ? 32u : 1u, 254u);
+                got = mode == 0 ? bbm::sqrt_short(b) : __builtin_amdgcn_sqrtf(b);
+                want = __builtin_sqrtf(b);
+            } else {
+                in = bbm::exp_in(b, 2u, 252u);
+                got = mode == 1 ? bbm::rcp_short<0>(b) : bbm::rcp_short<1>(b);
+                want = 1.0f / b;
+            }
+        }
+        if (in && bbm::f2u(got) != bbm::f2u(want)) {
+            bad++;
+            ea = bbm::f2u(a);
+            eb = bbm::f2u(b);
+        }
+    }
+    __shared__ uint32_t sbad[256], sa[256], sb[256];
+    sbad[threadIdx.x] = bad; sa[threadIdx.x] = ea; sb[threadIdx.x] = eb;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0, xa = 0, xb = 0;
+        for (int k = 0; k < 256; k++) {
+            t += sbad[k];
+            if (sbad[k]) { xa = sa[k]; xb = sb[k]; }
+        }
+        counts[blockIdx.x] = t;
+        ex[2 * blockIdx.x] = xa;
+        ex[2 * blockIdx.x + 1] = xb;
+    }
+}
+
+hipError_t launch_divsqrt_probe(int mode, uint64_t start, uint64_t count, uint32_t seed, uint32_t *counts,
+                                uint32_t *ex, int blocks, hipStream_t s)
+{
+    if (mode < 0 || mode > 5 || blocks <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_divsqrt_probe, dim3((unsigned)blocks), dim3(256), 0, s, mode, start, count, seed, counts, ex);
+    return hipGetLastError();
+}
+
 static inline dim3 grid_for(int64_t items, int block) { return dim3((unsigned)((items + block - 1) / block)); }
 
 template <int N>

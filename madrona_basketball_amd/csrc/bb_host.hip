@@ -1198,6 +1198,19 @@ int bb_diag_math(int32_t fn, const float *x, const float *y, float *out, int64_t
     return BB_OK;
 }
 
+// Diagnostic (not in the public header): bbm's short-path divide / square
+// root against the IEEE operations on the device (bb_common.hip
+// k_divsqrt_probe); counts[blocks] mismatches, ex[2 * blocks] one example each.
+int bb_diag_divsqrt(int32_t mode, uint64_t start, uint64_t count, uint32_t seed, uint32_t *counts, uint32_t *ex,
+                    int32_t blocks, int32_t gpu_id, void *stream)
+{
+    if (!counts || !ex || blocks <= 0 || mode < 0 || mode > 5) return fail(BB_ERR_INVALID_ARG, "bb_diag_divsqrt");
+    DeviceGuard g(gpu_id);
+    hipError_t e = bb::launch_divsqrt_probe(mode, start, count, seed, counts, ex, blocks, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "launch divsqrt probe");
+    return BB_OK;
+}
+
 // Diagnostic (not in the public header): one k_policy launch over `rows`
 // rows with per-wave phase clocks (bb_policy.hip pol_trace) copied to
 // out[waves][POL_TRACE_POINTS]; *waves = the launch's waves.

@@ -98,6 +98,9 @@ hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uin
 void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);
 // diagnostics: the step's scalar math on the device (bb_diag_math)
 hipError_t launch_math_probe(int fn, const float *x, const float *y, float *out, int64_t n, hipStream_t s);
+// diagnostics: bbm's short-path divide / square root vs IEEE (bb_diag_divsqrt)
+hipError_t launch_divsqrt_probe(int mode, uint64_t start, uint64_t count, uint32_t seed, uint32_t *counts,
+                                uint32_t *ex, int blocks, hipStream_t s);
 // streaming copy with the step's traffic mix (read_b, write_b bytes per item)
 hipError_t launch_stream_probe(const float4 *src, float4 *dst, int64_t items, int read_q, int write_q, int pattern,
                                int nt, hipStream_t s);

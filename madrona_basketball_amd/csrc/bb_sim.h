@@ -87,9 +87,9 @@ BB_HD F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }
 BB_HD F3 operator*(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
 BB_HD float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 BB_HD float len2(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-BB_HD float len(F3 a) { return bbm::sqrtf_(len2(a)); }
+BB_HD float len(F3 a) { return bbm::sqrt_(len2(a)); }
 // Vector3::normalize: unpinned Madrona detail, fixed as v * (1 / |v|).
-BB_HD F3 norm(F3 a) { return a * (1.0f / bbm::sqrtf_(len2(a))); }
+BB_HD F3 norm(F3 a) { return a * bbm::rcp_(bbm::sqrt_(len2(a))); }
 BB_HD F3 cross(F3 a, F3 b)
 {
     return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -141,15 +141,16 @@ BB_HD Q4 rotation_from_forward(F3 t)
     return quat_axis(bbm::acosf_(d), ax);
 }
 
-// getShotPointValue (src/helper.cpp:50-81)
-BB_HD int32_t shot_point_value(F3 p, F3 hz)
+// getShotPointValue (src/helper.cpp:50-81); arc_ge2: Params::arc_ge2 (the
+// distance test d >= ARC on the squared distance, no root)
+BB_HD int32_t shot_point_value(F3 p, F3 hz, float arc_ge2)
 {
-    const float d = len(p - hz);
+    const float d2 = len2(p - hz);
     if (p.y < CORNER_LO_Y || p.y > CORNER_HI_Y) {
         if (hz.x < HALF_WORLD_W) { if (p.x <= CORNER_LEFT_X) return 3; }
         else { if (p.x >= CORNER_RIGHT_X) return 3; }
     }
-    return d >= ARC ? 3 : 2;
+    return d2 >= arc_ge2 ? 3 : 2;
 }
 
 // c ? a : b, word by word for aggregates (a ?: on structs selects between
@@ -323,6 +324,15 @@ struct Params {
     Q4 start_q[2];               // angleAxis(-pi/2, z), angleAxis(+pi/2, z)     gen.cpp:196
     float rot_thresh;            // (float)acos(c) > pi/8  <=>  c < rot_thresh   game.cpp:746-747
     int32_t rot_exact;           // 1: threshold not verified, evaluate acos
+    // sqrtf is correctly rounded, hence monotone: sqrtf(t) <= c  <=>  t <= T
+    // with T the largest such float, and sqrtf(t) < c  <=>  t < T' with T'
+    // the smallest float whose root is >= c.  Distance tests against
+    // constants compare squared lengths with these (no root taken).
+    float grab_le2;              // len <= 0.3                                  game.cpp:202
+    float touch_le2;             // len <= AGENT_SIZE                           game.cpp:1045
+    float hoop_le2;              // sqrt(dx^2 + dy^2) <= HOOP_SCORE_ZONE_SIZE   game.cpp:885-888
+    float near_lt2;              // len < 2 (the shot's defender deviation)    game.cpp:329
+    float arc_ge2;               // len >= THREE_POINT_RADIUS                  helper.cpp:80
     uint32_t diag_skip;          // diagnostics only (MODE_SKIP): systems to leave out
     uint32_t diag_dup;           // diagnostics only (MODE_SKIP): systems to run twice
     uint32_t diag_keep;          // diagnostics only: 0 (the duplicate run's result is dropped)
@@ -430,8 +440,34 @@ BB_HD void store_f4(float *p, float a, float b, float c, float d)
 // same deterministic function the step would evaluate.
 inline bool rot_pred(float c) { return (float)bbm::acos_d((double)c) > PI_OVER_8; }
 
+// T(c) = the largest float t in [0, inf) with sqrtf(t) <= c; T'(c) = the
+// smallest with sqrtf(t) >= c (bisection over bit patterns: sqrtf is monotone)
+inline float sqrt_le_bound(float c)
+{
+    uint32_t lo = 0, hi = fbits(__builtin_inff());  // sqrtf(lo) <= c, sqrtf(hi) > c
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (bbm::sqrtf_(bitsf(mid)) <= c) lo = mid; else hi = mid;
+    }
+    return bitsf(lo);
+}
+inline float sqrt_ge_bound(float c)
+{
+    uint32_t lo = 0, hi = fbits(__builtin_inff());  // sqrtf(lo) < c, sqrtf(hi) >= c
+    while (hi - lo > 1u) {
+        const uint32_t mid = lo + (hi - lo) / 2u;
+        if (bbm::sqrtf_(bitsf(mid)) < c) lo = mid; else hi = mid;
+    }
+    return bitsf(hi);
+}
+
 inline void build_tables(Params &p)
 {
+    p.grab_le2 = sqrt_le_bound(0.3f);
+    p.touch_le2 = sqrt_le_bound(AGENT_SIZE);
+    p.hoop_le2 = sqrt_le_bound(HOOP_ZONE);
+    p.near_lt2 = sqrt_ge_bound(2.0f);
+    p.arc_ge2 = sqrt_ge_bound(ARC);
     for (int k = 0; k < 8; k++) bbm::sincosf_((float)k * ANGLE_STEP, &p.mv_sin[k], &p.mv_cos[k]);
     p.turn_q[0] = quat_axis_z(TURN_POS, 1.f);
     p.turn_q[1] = quat_axis_z(TURN_NEG, 1.f);
@@ -810,7 +846,7 @@ BB_HD MoveOut move_one(const MoveIn &in, const Params &p)
     else if (d <= 0.8f) { maxs *= .7f; dv = dv * .1f; }
     v = v + dv;
     if (in.has == 1) maxs *= BALL_SLOW;
-    if (len(v) > maxs) v = v * (maxs / len(v));
+    if (len(v) > maxs) v = v * bbm::div_(maxs, len(v));
     const float dx = v.x * TS, dy = v.y * TS;
     // the binding's grid is all-empty (src/bindings.cpp:7-11): the wall
     // lookup of game.cpp:472-484 always accepts the move.
@@ -835,7 +871,7 @@ BB_HD void sys_move_agents(World<N> &s, const Ctx &c, const A &ag)
 }
 
 template <int N>
-BB_HD void sys_grab(World<N> &s, int i)  // game.cpp:164-239
+BB_HD void sys_grab(World<N> &s, const Ctx &c, int i)  // game.cpp:164-239
 {
     if (s.msk[i][1] == 0 || s.act[i][3] == 0) return;
     s.cd[i] = 10.f;
@@ -846,7 +882,7 @@ BB_HD void sys_grab(World<N> &s, int i)  // game.cpp:164-239
         s.bid[i] = PH; s.has[i] = 0; s.holder = PH; s.grab = 0;
         return;
     }
-    if (len(s.bpos() - s.pos(i)) <= 0.3f) {
+    if (len2(s.bpos() - s.pos(i)) <= c.p->grab_le2) {  // len <= 0.3f
         if ((float)s.g_1v1 == 1.f && (float)s.team[i] != s.g_poss) {
             s.reset_now = 1;
             return;
@@ -896,6 +932,20 @@ BB_HD float nearest_opponent(const World<N> &s, int i)  // game.cpp:311-322
     return nd;
 }
 
+// nearest_opponent(s, i) < 2.0f without a root: some opponent's squared
+// distance below Params::near_lt2
+template <int N>
+BB_HD bool opponent_within_2(const World<N> &s, const Ctx &c, int i)
+{
+    const F3 pos = pick_by<N>(i, [&](int j) { return s.pos(j); });
+    const int32_t team = pick_by<N>(i, [&](int j) { return s.team[j]; });
+    bool near = false;
+#pragma unroll
+    for (int j = 0; j < N; j++)
+        if (s.team[j] != team && len2(pos - s.pos(j)) < c.p->near_lt2) near = true;
+    return near;
+}
+
 template <int N>
 BB_HD bool shoots(const World<N> &s, int i)
 {
@@ -903,10 +953,10 @@ BB_HD bool shoots(const World<N> &s, int i)
 }
 
 template <int N>
-BB_HD uint32_t shoot_draws(const World<N> &s, int i)  // uniforms agent i's shot consumes
+BB_HD uint32_t shoot_draws(const World<N> &s, const Ctx &c, int i)  // uniforms agent i's shot consumes
 {
     if (!shoots(s, i)) return 0u;
-    return 1u + (nearest_opponent(s, i) < 2.0f ? 1u : 0u) + (s.act[i][0] > 0 ? 1u : 0u);
+    return 1u + (opponent_within_2(s, c, i) ? 1u : 0u) + (s.act[i][0] > 0 ? 1u : 0u);
 }
 
 struct ShootOut {
@@ -930,7 +980,7 @@ BB_HD ShootOut shoot_one(const World<N> &s, const Ctx &c, int i)
     uint32_t ctr = s.rng_ctr;
 #pragma unroll
     for (int j = 0; j < N - 1; j++)
-        if (j < i) ctr += shoot_draws(s, j);
+        if (j < i) ctr += shoot_draws(s, c, j);
     auto draw = [&](float lo, float hi) { return sample_uniform_at(s, c, ctr++, lo, hi); };
     const F3 pos = pick_by<N>(i, [&](int j) { return s.pos(j); });
     const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
@@ -946,7 +996,7 @@ BB_HD ShootOut shoot_one(const World<N> &s, const Ctx &c, int i)
     float dev_def = 0.0f;
     const float nd = nearest_opponent(s, i);
     if (nd < 2.0f) {
-        const float sd = DEF_DEV / (nd + 0.1f);
+        const float sd = bbm::div_(DEF_DEV, nd + 0.1f);
         dev_def = draw(-sd, sd);
     }
     float dev_v = 0.0f;
@@ -962,7 +1012,7 @@ BB_HD ShootOut shoot_one(const World<N> &s, const Ctx &c, int i)
     if (!(along < 0.f)) o.going = (len2(ideal) - along * along <= radius * radius) ? 1 : 0;
     o.q = rotation_from_forward(o.fs);
     o.shot = 1;
-    if (s.holder == AGENT0_ID + i) o.value = shot_point_value(pos, target);
+    if (s.holder == AGENT0_ID + i) o.value = shot_point_value(pos, target, c.p->arc_ge2);
     return o;
 }
 
@@ -991,7 +1041,7 @@ BB_HD void sys_shoot(World<N> &s, const Ctx &c, const A &ag)
     // for another agent: only the holder's shot touches ball and possession)
     uint32_t draws = 0;
 #pragma unroll
-    for (int i = 0; i < N; i++) draws += shoot_draws(s, i);
+    for (int i = 0; i < N; i++) draws += shoot_draws(s, c, i);
     ag.template each<N>([&](int i) { return shoot_one(s, c, i); },
                         [&](int i, const ShootOut &o) { apply_shoot(s, i, o); });
     s.rng_ctr += draws;
@@ -1030,11 +1080,11 @@ BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
         }
     }
     const float ds = DIST_DEV * dh;
-    const float fs = DEF_DEV / nd + .0001f;
+    const float fs = bbm::div_(DEF_DEV, nd) + .0001f;
     const float vs = VEL_DEV * len(pick_by<N>(i, [&](int j) { return s.vel(j); }));
-    const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
-    const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
-    return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)), c.erf_tab);
+    const float sd = bbm::sqrt_(bbm::div_(ds * ds, 3.f) + bbm::div_(fs * fs, 3.f) + bbm::div_(vs * vs, 3.f));
+    const float z = bbm::div_(bbm::atanf_(bbm::div_(HOOP_ZONE, dh)), sd);
+    return (float)bbm::erf_d((double)bbm::div_(z, __builtin_sqrtf(2.f)), c.erf_tab);
 }
 
 template <int N, class A>
@@ -1050,7 +1100,7 @@ BB_HD void sys_score(World<N> &s, Ctx &c, int h)  // game.cpp:873-953
     const F3 hp = hoop_pos<N>(c, h);
     const int32_t hid = h == 0 ? HOOP0_ID : HOOP1_ID;
     const float dx = s.bx - hp.x, dy = s.by - hp.y;
-    if (!(bbm::sqrtf_(dx * dx + dy * dy) <= HOOP_ZONE && (float)s.fl == 1.f)) return;
+    if (!((dx * dx + dy * dy) <= c.p->hoop_le2 && (float)s.fl == 1.f)) return;  // sqrt(..) <= HOOP_ZONE
     const int32_t pts = s.spv;
     int32_t inb_team = 0;
 #pragma unroll
@@ -1103,11 +1153,11 @@ BB_HD void sys_out_of_bounds(World<N> &s, Ctx &c)  // game.cpp:1055-1113
 }
 
 template <int N>
-BB_HD void sys_last_touch(World<N> &s)  // game.cpp:1034-1051
+BB_HD void sys_last_touch(World<N> &s, const Ctx &c)  // game.cpp:1034-1051
 {
 #pragma unroll
-    for (int i = 0; i < N; i++)
-        if (len(s.bpos() - s.pos(i)) <= AGENT_SIZE) { s.lta = AGENT0_ID + i; s.ltt = s.team[i]; }
+    for (int i = 0; i < N; i++)  // len <= AGENT_SIZE
+        if (len2(s.bpos() - s.pos(i)) <= c.p->touch_le2) { s.lta = AGENT0_ID + i; s.ltt = s.team[i]; }
 }
 
 template <int N>
@@ -1153,8 +1203,8 @@ BB_HD int32_t points_worth_one(const World<N> &s, const Ctx &c, int i)
     // first hoop (creation order) that is not defended; both are never defended at once
     const F3 p = pick_by<N>(i, [&](int j) { return s.pos(j); });
     const int32_t dhoop = pick_by<N>(i, [&](int j) { return s.dhoop[j]; });
-    if (HOOP0_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 0));
-    if (HOOP1_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 1));
+    if (HOOP0_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 0), c.p->arc_ge2);
+    if (HOOP1_ID != dhoop) return shot_point_value(p, hoop_pos<N>(c, 1), c.p->arc_ge2);
     return 2;
 }
 
@@ -1607,10 +1657,10 @@ BB_HD void shared_obs_prepare(const World<N> &s, const Ctx &c, SharedObs<N> &sh)
             const F3 to = s.pos(j) - s.pos(a), back = s.pos(a) - s.pos(j);
             const float l2 = len2(to);                        // == len2(back) exactly
             const bool nz = l2 > 1e-6f;
-            const float r = 1.0f / bbm::sqrtf_(l2);           // the factor norm() applies
+            const float r = bbm::rcp_(bbm::sqrt_(l2));        // the factor norm() applies
             sh.rdir[a][j] = nz ? to * r : f3(0.f, 0.f, 0.f);
             sh.rdir[j][a] = nz ? back * r : f3(0.f, 0.f, 0.f);  // not -(to * r): +0 stays +0
-            sh.rlen[a][j] = sh.rlen[j][a] = bbm::sqrtf_(l2);
+            sh.rlen[a][j] = sh.rlen[j][a] = bbm::sqrt_(l2);
         }
 }
 
@@ -1663,10 +1713,10 @@ BB_HD void emit_row_view(const World<N> &s, const Ctx &c, int a, IntrOf intr, bo
         const int j = view_source<N>(t, a);
         const F3 pj = s.pos(j), to = pj - p;
         const float l2 = len2(to);
-        const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
+        const float r = bbm::rcp_(bbm::sqrt_(l2));  // the factor norm() applies
         o.put3(pj);
         o.put3(l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f));
-        o.put(bbm::sqrtf_(l2));
+        o.put(bbm::sqrt_(l2));
         if (share) {
 #pragma unroll
             for (int q = 0; q < INTRINSIC; q++) o.put(intr(j, q));
@@ -1756,7 +1806,7 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t s
     BB_RUN(2, sys_action_mask(s, flags))
     BB_RUN(3, sys_move_agents(s, c, ag))
     ag.mark(2);
-    BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, i))
+    BB_RUN(4, for (int i = 0; i < N; i++) sys_grab(s, c, i))
     BB_RUN(5, for (int i = 0; i < N; i++) sys_pass(s, i))
     BB_RUN(6, sys_shoot(s, c, ag))
     ag.mark(3);
@@ -1765,7 +1815,7 @@ BB_HD void step_world_pre_obs(World<N> &s, Ctx &c, const A &ag = A(), uint32_t s
     BB_RUN(9, sys_score(s, c, 0); sys_score(s, c, 1))   // hoop 0, then hoop 1
     ag.mark(4);
     BB_RUN(10, sys_out_of_bounds(s, c))
-    BB_RUN(11, sys_last_touch(s))
+    BB_RUN(11, sys_last_touch(s, c))
     BB_RUN(12, sys_clock(s))
     BB_RUN(13, sys_inbound_violation(s, c))
     ag.mark(5);

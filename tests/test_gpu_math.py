@@ -91,3 +91,52 @@ def test_device_atan2f_equals_host_build(dev):
         b = host_eval(P, "bb_atan2f", x, y)  # bb_atan2f(y, x) = atan2f_(y, x)
         ok = same(a, b)
         assert ok.all(), (y[~ok][:3], x[~ok][:3])
+
+
+# bb_diag_divsqrt modes (bb_common.hip k_divsqrt_probe)
+DIVSQRT = {"sqrt_short": 0, "rcp_refined": 1, "rcp_short1": 2, "div_short1": 3, "div_short2": 4, "v_sqrt_f32": 5}
+
+
+def divsqrt_mismatches(L, mode, start, count, seed=0, blocks=8192):
+    L.bb_diag_divsqrt.restype = ctypes.c_int
+    L.bb_diag_divsqrt.argtypes = [ctypes.c_int32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_void_p]
+    counts = torch.zeros(blocks, dtype=torch.int32, device="cuda")
+    ex = torch.zeros(2 * blocks, dtype=torch.int32, device="cuda")
+    rc = L.bb_diag_divsqrt(mode, start, count, seed, counts.data_ptr(), ex.data_ptr(), blocks, 0,
+                           torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, L.bb_last_error()
+    torch.cuda.synchronize()
+    c = counts.cpu().numpy().astype(np.int64)
+    e = ex.cpu().numpy().view(np.uint32).reshape(-1, 2)
+    bad = int(c.sum())
+    examples = [(hex(a), hex(b)) for a, b in e[c > 0][:4]]
+    return bad, examples
+
+
+@pytest.mark.parametrize("name", ["sqrt_short", "rcp_short1"])
+def test_short_path_divide_sqrt_equal_ieee_on_every_input(dev, name):
+    """bbm::sqrt_ and bbm::rcp_'s short paths == the IEEE operations (hipcc's
+    correctly rounded expansions) on every float of their ranges (2^32
+    patterns, the rest skipped)."""
+    bad, ex = divsqrt_mismatches(dev, DIVSQRT[name], 0, 2**32)
+    assert bad == 0, (name, bad, ex)
+
+
+def test_short_path_quotient_equals_ieee(dev):
+    """bbm::div_'s short path == a / b on 2^36 pseudo-random operand pairs
+    with both exponents in its range."""
+    for seed in range(16):
+        bad, ex = divsqrt_mismatches(dev, DIVSQRT["div_short2"], 0, 2**32, seed=seed)
+        assert bad == 0, (seed, bad, ex)
+
+
+def test_divsqrt_variants_report(dev):
+    """Which cheaper sequences would also be exact (reported, not asserted):
+    the bare v_sqrt_f32, the refined reciprocal alone, Markstein's single
+    correction."""
+    out = {}
+    for name in ("v_sqrt_f32", "rcp_refined"):
+        out[name] = divsqrt_mismatches(dev, DIVSQRT[name], 0, 2**32)
+    out["div_short1"] = divsqrt_mismatches(dev, DIVSQRT["div_short1"], 0, 2**32, seed=99)
+    print("divsqrt variants:", out)
