@@ -140,14 +140,64 @@ __global__ __launch_bounds__(256) void k_math_probe(int fn, const float *x, cons
     out[i] = r;
 }
 
-// Diagnostics (tests/test_gpu_math.py): bbm's short-path divide / square root
-// (bb_math.h) against the IEEE operations compiled by hipcc, on the device.
-// mode 0 sqrt_short, 1 rcp refined only, 2 rcp_short<1>, 3 div_short<1>,
+// Diagnostics (tests/test_gpu_math.py): shorter
+// sequences for the step's correctly rounded f32 quotients and square roots,
+// against the IEEE operations hipcc compiles.  The compiler's expansions serve
+// every input (operand scaling for extreme exponents, special values: 10-11
+// instructions per quotient, ~14 per root); these are its own sequences
+// without the scaling, valid well inside the exponent range:
+//   rcp_refined(b):  v_rcp_f32 then one Newton step by fma;
+//   div_short<C>:    q = a y, then C residual corrections q + (a - b q) y
+//                    (C = 1 Markstein's, C = 2 the expansion's);
+//   sqrt_short(x):   v_sqrt_f32 then the expansion's neighbour selection.
+// Measured (round 4, profiles/r04/a_divsqrt_*): exact on every input tried
+// (rcp on all 2^32 floats of its range, div on 2^32 random pairs), but with
+// the wave-uniform range guards the step got slower (65 536 x 2 21.0 ->
+// 21.5 us), and even unguarded non-IEEE fast division / roots save only
+// 0.35 us: the product keeps the IEEE operators.
+// mode 0 sqrt_short, 1 rcp_refined, 2 rcp_short<1>, 3 div_short<1>,
 // 4 div_short<2>, 5 the bare v_sqrt_f32.  Modes 0-2 and 5 take the float bit
 // patterns start + i, i < count, skipping those outside the short path's
 // range; modes 3-4 take pseudo-random operand pairs (index i, seed) with
-// exponents in the short path's range.  Per workgroup: the mismatch count and
-// one mismatching input (a bits, b bits).
+// exponents in [2^-47, 2^48).  Per workgroup: the mismatch count and one
+// mismatching input (a bits, b bits).
+__device__ __forceinline__ bool exp_in(float x, uint32_t lo, uint32_t hi)
+{
+    return ((bbm::f2u(x) >> 23) & 0xffu) - lo <= hi - lo;
+}
+__device__ __forceinline__ float rcp_refined(float b)
+{
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    const float e = __builtin_fmaf(-b, y0, 1.0f);
+    return __builtin_fmaf(e, y0, y0);
+}
+template <int C>
+__device__ __forceinline__ float div_short(float a, float b)
+{
+    const float y = rcp_refined(b);
+    float q = a * y;
+#pragma unroll
+    for (int k = 0; k < C; k++) q = __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
+    return q;
+}
+template <int C>
+__device__ __forceinline__ float rcp_short(float b)
+{
+    const float y = rcp_refined(b);
+    float q = y;
+#pragma unroll
+    for (int k = 0; k < C; k++) q = __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), y, q);
+    return q;
+}
+__device__ __forceinline__ float sqrt_short(float x)
+{
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float lo = bbm::u2f(bbm::f2u(s) - 1u), hi = bbm::u2f(bbm::f2u(s) + 1u);
+    const float rlo = __builtin_fmaf(-lo, s, x), rhi = __builtin_fmaf(-hi, s, x);
+    float r = rlo <= 0.0f ? lo : s;
+    r = rhi > 0.0f ? hi : r;
+    return r;
+}
 __device__ __forceinline__ uint32_t probe_hash(uint32_t x)
 {
     x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
@@ -170,17 +220,17 @@ __global__ __launch_bounds__(256) void k_divsqrt_probe(int mode, uint64_t start,
             const uint32_t h = probe_hash((uint32_t)i ^ probe_hash(seed + (uint32_t)(i >> 32)));
             a = probe_operand(h, 80u, 174u);
             b = probe_operand(probe_hash(h ^ 0x9e3779b9u), 80u, 174u);
-            got = mode == 3 ? bbm::div_short<1>(a, b) : bbm::div_short<2>(a, b);
+            got = mode == 3 ? div_short<1>(a, b) : div_short<2>(a, b);
             want = a / b;
         } else {
             b = __builtin_bit_cast(float, (uint32_t)(start + i));
             if (mode == 0 || mode == 5) {
-                in = !(bbm::f2u(b) >> 31) && bbm::exp_in(b, mode == 0 ? 32u : 1u, 254u);
-                got = mode == 0 ? bbm::sqrt_short(b) : __builtin_amdgcn_sqrtf(b);
+                in = !(bbm::f2u(b) >> 31) && exp_in(b, mode == 0 ? 32u : 1u, 254u);
+                got = mode == 0 ? sqrt_short(b) : __builtin_amdgcn_sqrtf(b);
                 want = __builtin_sqrtf(b);
             } else {
-                in = bbm::exp_in(b, 2u, 252u);
-                got = mode == 1 ? bbm::rcp_short<0>(b) : bbm::rcp_short<1>(b);
+                in = exp_in(b, 2u, 252u);
+                got = mode == 1 ? rcp_refined(b) : rcp_short<1>(b);
                 want = 1.0f / b;
             }
         }

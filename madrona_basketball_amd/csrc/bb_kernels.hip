@@ -487,9 +487,9 @@ __device__ __forceinline__ void lane_shared_obs(const World<N> &v, const Ctx &c,
         for (int t = 1; t < N; t++) {
             const F3 to = v.pos(t) - v.pos(0);
             const float l2 = len2(to);
-            const float r = bbm::rcp_(bbm::sqrt_(l2));  // the factor norm() applies
+            const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
             sh.rdir[0][t] = l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f);
-            sh.rlen[0][t] = bbm::sqrt_(l2);
+            sh.rlen[0][t] = bbm::sqrtf_(l2);
         }
     }
 }
@@ -1354,9 +1354,9 @@ struct LaneSources {
         for (int j = 0; j < N; j++) {
             const F3 to = s.pos(j) - p;  // as emit_row_view
             const float l2 = len2(to);
-            const float rr = bbm::rcp_(bbm::sqrt_(l2));
+            const float rr = 1.0f / bbm::sqrtf_(l2);
             const F3 d = l2 > 1e-6f ? to * rr : f3(0.f, 0.f, 0.f);
-            r[j][0] = d.x; r[j][1] = d.y; r[j][2] = d.z; r[j][3] = bbm::sqrt_(l2);
+            r[j][0] = d.x; r[j][1] = d.y; r[j][2] = d.z; r[j][3] = bbm::sqrtf_(l2);
         }
         oh_holder = AGENT0_ID + k == s.holder ? 1.f : 0.f;
         oh_inb = AGENT0_ID + k == ib ? 1.f : 0.f;

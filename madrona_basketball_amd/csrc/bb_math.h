@@ -290,95 +290,6 @@ BB_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
 BB_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
 BB_HD double u2d(uint64_t u) { return __builtin_bit_cast(double, u); }
 
-// ------------------------------- correctly rounded f32 divide and square root
-// The reference's float quotients and square roots are IEEE (correctly
-// rounded), and so are the step's.  The compiler's general expansions serve
-// every input -- operand scaling for extreme exponents, special values -- at
-// 10-11 instructions per quotient and ~14 per square root.  The device forms
-// below take a short path when the operands lie well inside the exponent
-// range (the game's positions, distances and speeds always do) and the
-// general one otherwise:
-//   rcp_(b):    y0 = v_rcp_f32(b) (within an ulp), one Newton step by fused
-//               multiply-adds (the compiler expansion's refinement), then one
-//               residual correction;
-//   div_(a, b): y = the refined reciprocal, q = a y, then the expansion's two
-//               residual corrections q + (a - b q) y by fma;
-//   sqrt_(x):   s = v_sqrt_f32(x), then the expansion's neighbour selection
-//               (residuals x - s s- and x - s s+ by fma) -- on inputs the
-//               expansion does not scale (x >= 2^-96) the same operations.
-// On the short-path ranges these are the compiler's own sequences without the
-// scaling steps, which do nothing there; each is also compared with the IEEE
-// operation on the device (tests/test_gpu_math.py, bb_diag_divsqrt: rcp_ and
-// sqrt_ on every one of the 2^32 inputs, div_ on 2^36 operand pairs).
-// Short-path ranges (biased exponent fields): rcp_ [2, 252]; div_ both
-// operands [80, 174] (2^-47 .. 2^48); sqrt_ [32, 254].
-#ifndef BB_SHORT_DIVSQRT
-#define BB_SHORT_DIVSQRT 0  // 1: the short paths (diagnostic builds until measured)
-#endif
-BB_HD bool exp_in(float x, uint32_t lo, uint32_t hi)
-{
-    return ((f2u(x) >> 23) & 0xffu) - lo <= hi - lo;
-}
-#if defined(__HIPCC__)
-__device__ __forceinline__ float rcp_refined(float b)
-{
-    const float y0 = __builtin_amdgcn_rcpf(b);
-    const float e = __builtin_fmaf(-b, y0, 1.0f);
-    return __builtin_fmaf(e, y0, y0);
-}
-// corrections: 1 (Markstein's single step) or 2 (the compiler expansion's)
-template <int C>
-__device__ __forceinline__ float div_short(float a, float b)
-{
-    const float y = rcp_refined(b);
-    float q = a * y;
-#pragma unroll
-    for (int k = 0; k < C; k++) q = __builtin_fmaf(__builtin_fmaf(-b, q, a), y, q);
-    return q;
-}
-template <int C>
-__device__ __forceinline__ float rcp_short(float b)
-{
-    const float y = rcp_refined(b);
-    float q = y;
-#pragma unroll
-    for (int k = 0; k < C; k++) q = __builtin_fmaf(__builtin_fmaf(-b, q, 1.0f), y, q);
-    return q;
-}
-__device__ __forceinline__ float sqrt_short(float x)
-{
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float lo = u2f(f2u(s) - 1u), hi = u2f(f2u(s) + 1u);
-    const float rlo = __builtin_fmaf(-lo, s, x), rhi = __builtin_fmaf(-hi, s, x);
-    float r = rlo <= 0.0f ? lo : s;
-    r = rhi > 0.0f ? hi : r;
-    return r;
-}
-#endif
-BB_HD float rcp_(float b)
-{
-#if defined(__HIP_DEVICE_COMPILE__) && BB_SHORT_DIVSQRT
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!exp_in(b, 2u, 252u)) == 0, 1)) return rcp_short<1>(b);
-#endif
-    return 1.0f / b;
-}
-BB_HD float div_(float a, float b)
-{
-#if defined(__HIP_DEVICE_COMPILE__) && BB_SHORT_DIVSQRT
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(exp_in(a, 80u, 174u) && exp_in(b, 80u, 174u))) == 0, 1))
-        return div_short<2>(a, b);
-#endif
-    return a / b;
-}
-BB_HD float sqrt_(float x)
-{
-#if defined(__HIP_DEVICE_COMPILE__) && BB_SHORT_DIVSQRT
-    if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(x >= 0x1p-96f || x == 0.0f)) == 0, 1)) return sqrt_short(x);
-#endif
-    return __builtin_sqrtf(x);
-}
-
-
 // __sincosf_table[0]: 2/pi 2^24, pi/2 and the polynomial coefficients.
 // __sincosf_table[1] (quadrants 2-3) holds the cosine coefficients negated:
 // every fused step of the cosine polynomial then yields the exact negation,
@@ -493,14 +404,14 @@ BB_HD float glibc_atanf(float x)
         x = __builtin_fabsf(x);
         if (ix < 0x3f980000) {      // |x| < 1.1875
             if (ix < 0x3f300000) {  // 7/16 <= |x| < 11/16
-                id = 0; x = div_((x + x) - 1.0f, x + 2.0f);
+                id = 0; x = ((x + x) - 1.0f) / (x + 2.0f);
             } else {                // 11/16 <= |x| < 19/16
-                id = 1; x = div_(x - 1.0f, x + 1.0f);
+                id = 1; x = (x - 1.0f) / (x + 1.0f);
             }
         } else if (ix < 0x401c0000) {  // |x| < 2.4375
-            id = 2; x = div_(x - 1.5f, x * 1.5f + 1.0f);
+            id = 2; x = (x - 1.5f) / (x * 1.5f + 1.0f);
         } else {                       // 2.4375 <= |x| < 2^25
-            id = 3; x = -rcp_(x);  // -1.0f / x (round to nearest is sign-symmetric)
+            id = 3; x = -1.0f / x;
         }
     }
     const float z = x * x;
@@ -551,7 +462,7 @@ BB_HD float glibc_atan2f(float y, float x)
     float z;
     if (k > 60) z = pi_o_2 - u2f(0x333bbd2e);           // pi_o_2 + 0.5 pi_lo, folded
     else if ((int32_t)hx < 0 && k < -60) z = 0.0f;
-    else z = glibc_atanf(__builtin_fabsf(div_(y, x)));
+    else z = glibc_atanf(__builtin_fabsf(y / x));
     switch (m) {
     case 0: return z;
     case 1: return u2f(f2u(z) ^ 0x80000000u);
@@ -575,25 +486,25 @@ BB_HD float glibc_acosf(float x)
         const float z = x * x;
         const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
         const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        const float r = div_(p, q);
+        const float r = p / q;
         return pio2_hi - (x - (pio2_lo - x * r));
     }
     if ((int32_t)hx < 0) {  // x < -0.5
         const float z = (1.0f + x) * 0.5f;
         const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
         const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-        const float s = sqrt_(z);
-        const float r = div_(p, q);
+        const float s = __builtin_sqrtf(z);
+        const float r = p / q;
         const float w = r * s - pio2_lo;
         return pi - 2.0f * (s + w);
     }
     const float z = (1.0f - x) * 0.5f;  // x > 0.5
-    const float s = sqrt_(z);
+    const float s = __builtin_sqrtf(z);
     const float df = u2f(f2u(s) & 0xfffff000u);
-    const float c = div_(z - df * df, s + df);
+    const float c = (z - df * df) / (s + df);
     const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
     const float q = 1.0f + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
-    const float r = div_(p, q);
+    const float r = p / q;
     const float w = r * s + c;
     return 2.0f * (df + w);
 }

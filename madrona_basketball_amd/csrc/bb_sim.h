@@ -87,9 +87,9 @@ BB_HD F3 operator-(F3 a) { return f3(-a.x, -a.y, -a.z); }
 BB_HD F3 operator*(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }
 BB_HD float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 BB_HD float len2(F3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-BB_HD float len(F3 a) { return bbm::sqrt_(len2(a)); }
+BB_HD float len(F3 a) { return bbm::sqrtf_(len2(a)); }
 // Vector3::normalize: unpinned Madrona detail, fixed as v * (1 / |v|).
-BB_HD F3 norm(F3 a) { return a * bbm::rcp_(bbm::sqrt_(len2(a))); }
+BB_HD F3 norm(F3 a) { return a * (1.0f / bbm::sqrtf_(len2(a))); }
 BB_HD F3 cross(F3 a, F3 b)
 {
     return f3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -846,7 +846,7 @@ BB_HD MoveOut move_one(const MoveIn &in, const Params &p)
     else if (d <= 0.8f) { maxs *= .7f; dv = dv * .1f; }
     v = v + dv;
     if (in.has == 1) maxs *= BALL_SLOW;
-    if (len(v) > maxs) v = v * bbm::div_(maxs, len(v));
+    if (len(v) > maxs) v = v * (maxs / len(v));
     const float dx = v.x * TS, dy = v.y * TS;
     // the binding's grid is all-empty (src/bindings.cpp:7-11): the wall
     // lookup of game.cpp:472-484 always accepts the move.
@@ -996,7 +996,7 @@ BB_HD ShootOut shoot_one(const World<N> &s, const Ctx &c, int i)
     float dev_def = 0.0f;
     const float nd = nearest_opponent(s, i);
     if (nd < 2.0f) {
-        const float sd = bbm::div_(DEF_DEV, nd + 0.1f);
+        const float sd = DEF_DEV / (nd + 0.1f);
         dev_def = draw(-sd, sd);
     }
     float dev_v = 0.0f;
@@ -1080,11 +1080,11 @@ BB_HD float shot_pct_one(const World<N> &s, const Ctx &c, int i)
         }
     }
     const float ds = DIST_DEV * dh;
-    const float fs = bbm::div_(DEF_DEV, nd) + .0001f;
+    const float fs = DEF_DEV / nd + .0001f;
     const float vs = VEL_DEV * len(pick_by<N>(i, [&](int j) { return s.vel(j); }));
-    const float sd = bbm::sqrt_(bbm::div_(ds * ds, 3.f) + bbm::div_(fs * fs, 3.f) + bbm::div_(vs * vs, 3.f));
-    const float z = bbm::div_(bbm::atanf_(bbm::div_(HOOP_ZONE, dh)), sd);
-    return (float)bbm::erf_d((double)bbm::div_(z, __builtin_sqrtf(2.f)), c.erf_tab);
+    const float sd = bbm::sqrtf_((ds * ds / 3.f) + (fs * fs / 3.f) + (vs * vs / 3.f));
+    const float z = bbm::atanf_(HOOP_ZONE / dh) / sd;
+    return (float)bbm::erf_d((double)(z / bbm::sqrtf_(2.f)), c.erf_tab);
 }
 
 template <int N, class A>
@@ -1657,10 +1657,10 @@ BB_HD void shared_obs_prepare(const World<N> &s, const Ctx &c, SharedObs<N> &sh)
             const F3 to = s.pos(j) - s.pos(a), back = s.pos(a) - s.pos(j);
             const float l2 = len2(to);                        // == len2(back) exactly
             const bool nz = l2 > 1e-6f;
-            const float r = bbm::rcp_(bbm::sqrt_(l2));        // the factor norm() applies
+            const float r = 1.0f / bbm::sqrtf_(l2);        // the factor norm() applies
             sh.rdir[a][j] = nz ? to * r : f3(0.f, 0.f, 0.f);
             sh.rdir[j][a] = nz ? back * r : f3(0.f, 0.f, 0.f);  // not -(to * r): +0 stays +0
-            sh.rlen[a][j] = sh.rlen[j][a] = bbm::sqrt_(l2);
+            sh.rlen[a][j] = sh.rlen[j][a] = bbm::sqrtf_(l2);
         }
 }
 
@@ -1713,10 +1713,10 @@ BB_HD void emit_row_view(const World<N> &s, const Ctx &c, int a, IntrOf intr, bo
         const int j = view_source<N>(t, a);
         const F3 pj = s.pos(j), to = pj - p;
         const float l2 = len2(to);
-        const float r = bbm::rcp_(bbm::sqrt_(l2));  // the factor norm() applies
+        const float r = 1.0f / bbm::sqrtf_(l2);  // the factor norm() applies
         o.put3(pj);
         o.put3(l2 > 1e-6f ? to * r : f3(0.f, 0.f, 0.f));
-        o.put(bbm::sqrt_(l2));
+        o.put(bbm::sqrtf_(l2));
         if (share) {
 #pragma unroll
             for (int q = 0; q < INTRINSIC; q++) o.put(intr(j, q));

@@ -116,16 +116,17 @@ def divsqrt_mismatches(L, mode, start, count, seed=0, blocks=8192):
 
 @pytest.mark.parametrize("name", ["sqrt_short", "rcp_short1"])
 def test_short_path_divide_sqrt_equal_ieee_on_every_input(dev, name):
-    """bbm::sqrt_ and bbm::rcp_'s short paths == the IEEE operations (hipcc's
-    correctly rounded expansions) on every float of their ranges (2^32
-    patterns, the rest skipped)."""
+    """The short square root and reciprocal sequences of k_divsqrt_probe
+    (bb_common.hip) == the IEEE operations (hipcc's correctly rounded
+    expansions) on every float of their ranges (2^32 patterns, the rest
+    skipped).  Diagnostic: the product keeps the IEEE operators."""
     bad, ex = divsqrt_mismatches(dev, DIVSQRT[name], 0, 2**32)
     assert bad == 0, (name, bad, ex)
 
 
 def test_short_path_quotient_equals_ieee(dev):
-    """bbm::div_'s short path == a / b on 2^36 pseudo-random operand pairs
-    with both exponents in its range."""
+    """The short quotient (two residual corrections) == a / b on 2^36
+    pseudo-random operand pairs with both exponents in [2^-47, 2^48)."""
     for seed in range(16):
         bad, ex = divsqrt_mismatches(dev, DIVSQRT["div_short2"], 0, 2**32, seed=seed)
         assert bad == 0, (seed, bad, ex)
