@@ -402,9 +402,23 @@ def main():
             wall2 = time.perf_counter() - t0
             ev = sum(pol2.rollout(sim2, K2, b2, seed=args.seed, step0=(2 + rollouts + i) * K2, time_kernels=True)
                      for i in range(rollouts)) / rollouts
+            # algorithmic bytes per PPO step: the world step's B(2) plus per
+            # trainee row the policy's observation read (128 floats), the
+            # buffer.obs record, the action row into the action tensor and
+            # into buffer.actions, log-prob, value, and the reward / done read
+            # from the sim and recorded (ppo.py:129-134)
+            per_row = 4 * 128 * 2 + 24 * 2 + 4 * 2 + 8 * 2
+            step_bytes = W2 * (L0.bb_algorithmic_bytes_per_world(2) + per_row)
+            us_step = ev * 1e3 / K2
             line = {"worlds": W2, "agents": 2, "rollout": K2, "rollouts": rollouts,
                     "value": W2 * K2 * rollouts / wall2, "unit": "env-steps/s",
                     "us_per_step": wall2 * 1e6 / (K2 * rollouts), "rollout_avg_us_events": ev * 1e3,
+                    "roofline": {"bound": "hbm", "scope": "whole PPO step (policy pass + world step + records)",
+                                 "algorithmic_bytes_per_step": step_bytes,
+                                 "achieved": step_bytes / us_step / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": step_bytes / us_step / 1e3 / HBM_PEAK_GBS,
+                                 "mfma_flops_per_step": W2 * 2 * (128 * 32 + 32 * 32 + 32 * 20),
+                                 "traffic": load_traffic(f"W{W2}_PPO_R{K2}")},
                     "what": "bb_rollout_policy: per step the fused policy acts for agent 0 of every world, the "
                             "step, obs/actions/log-probs/values/rewards/dones recorded ([K, W, ...]); then the "
                             "next-value pass (scripts/ppo.py:61-141)"}
