@@ -477,11 +477,11 @@ def main():
                            f"of every step recorded into [{K}, W, N, ...] buffers" if K and not args.policy
                            else ("" if K else "; one step per call"))
                         + ((f"; PPO's rollout on the device (bb_rollout_policy: per step the fused policy "
-                            f"-- reference Agent layout, random init, Gumbel sampling -- acts for agent 0, the "
+                            f"-- reference Agent layout, random init, categorical sampling -- acts for agent 0, the "
                             f"step, and obs/actions/log-probs/values/rewards/dones recorded into [{K}, W, ...] "
                             f"buffers; agent 1 by the in-sim defence AI; the staged random rows are unused)"
                             if K else "; actions from the fused policy (reference Agent layout, random init, "
-                            "Gumbel sampling) for every agent before each step") if args.policy else ""),
+                            "categorical sampling) for every agent before each step") if args.policy else ""),
             "worlds_per_gpu": W,
             "total_worlds": total_worlds,
             "agents_per_world": args.agents,

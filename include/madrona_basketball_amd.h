@@ -219,8 +219,10 @@ typedef struct bb_policy_weights {
  * aligned), writes 6 int32 actions to actions + r * action_stride (e.g. the
  * action tensor's column of one agent), and optionally log_prob[r] (sum over
  * the buckets) and value[r].  stochastic = 0: per-bucket argmax (best(),
- * scripts/action.py:21-23); 1: Gumbel-max sample keyed threefry({seed, step},
- * {r, logit}).  gpu_id: the device of the pointers (CUDA mode). */
+ * scripts/action.py:21-23); 1: a categorical sample (Categorical.sample,
+ * action.py:29-33) by inverse CDF, bucket b's uniform from threefry({seed,
+ * step}, {r, b >> 1}) word b & 1.  gpu_id: the device of the pointers (CUDA
+ * mode). */
 int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu_id, const float *obs,
                       int64_t rows, int64_t obs_stride, int32_t *actions, int64_t action_stride, float *log_prob,
                       float *value, int32_t stochastic, uint32_t seed, uint32_t step, void *stream);

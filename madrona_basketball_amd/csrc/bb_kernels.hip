@@ -1091,7 +1091,7 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     a.stochastic = r.stochastic;
     a.seed = r.seed;
     auto bar = [] { lds_barrier(); };
-    // the Gumbel noise of a step depends on (seed, step, row, logit) only: each
+    // the sampling uniforms of a step depend on (seed, step, row, bucket) only: each
     // step's is drawn while the sim wave runs the step before it
     BucketNoise<8> noise;
     if (r.stochastic) bucket_noise<8>(noise, r.seed, r.step0, row0 + rh, W, lane);
@@ -1129,7 +1129,7 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             if (pw == 0) ppo_trace(r, t, 3);
             lds_barrier();  // actions in LDS
             // while the sim wave steps: buffer.obs[t] = X (this wave's 8 rows),
-            // then the next step's Gumbel noise
+            // then the next step's sampling uniforms
             if (r.obs_out) {
                 for (int i = lane; i < 8 * 32; i += WAVE) {
                     const int rr = r0 + rh + i / 32, qq = i % 32;

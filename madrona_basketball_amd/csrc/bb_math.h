@@ -157,7 +157,7 @@ BB_HD double exp_d(double x)
     return ldexp_d(p, (int)k);
 }
 
-// log (the policy's logsumexp and Gumbel noise, bb_policy.h): x = m 2^e with
+// log (double; the policy's own f32 log is pol_logf, bb_policy.h): x = m 2^e with
 // m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(s), s = (m - 1)/(m + 1), |s| <= 0.1716:
 // odd series to s^25 (next term < 2^-60).
 BB_HD double log_d(double x)

@@ -7,7 +7,8 @@
 //   h1 = relu(LN(W1 x + b1)),  h2 = relu(LN(W2 h1 + b2))       backbone, agent.py:115-124
 //   logits = Wa h2 + ba (19),  value = Wc h2 + bc              heads, agent.py:127-128
 //   per bucket [2,8,3,2,2,2] (env.py:102): action = argmax (best(), action.py:21-23) or a
-//   Gumbel-max sample; log_prob = logit - logsumexp (Categorical, action.py:16-33), summed.
+//   categorical sample (inverse CDF of softmax); log_prob = logit - logsumexp (Categorical,
+//   action.py:16-33), summed.
 //
 // Arithmetic order (fixed, -ffp-contract=off): each matrix product is the k-ordered
 // fmaf chain the gfx950 f32 MFMA computes (v_mfma_f32_16x16x4_f32: one rounding per
@@ -44,7 +45,7 @@ struct PolicyArgs {
     int64_t act_stride;    // int32 words
     float *log_prob;       // [rows] (optional)
     float *value;          // [rows] (optional)
-    int32_t stochastic;    // 0: argmax (best), 1: Gumbel-max sample
+    int32_t stochastic;    // 0: argmax (best), 1: categorical sample (inverse CDF)
     uint32_t seed, step;   // sample key: threefry({seed, step}, {row, logit})
     // actions == nullptr: no actions written (value only, agent.evaluate).
     // Rollout recording (bb_rollout_policy, scripts/ppo.py:129-134; all optional):
@@ -114,14 +115,34 @@ BB_HD float pol_logf(float x)
 BB_HD float pol_clamp(float x) { return __builtin_fminf(__builtin_fmaxf(x, -5.f), 5.f); }  // v_max / v_min
 BB_HD float pol_relu(float x) { return x > 0.f ? x : 0.f; }
 
-// Gumbel noise of logit i of row r: -log(-log(u)), u in (0, 1); one threefry
-// call serves logits 2p and 2p + 1 (its two output words).
-BB_HD float pol_u01_open(uint32_t bits) { return ((float)(bits >> 8) + 0.5f) * (1.0f / 16777216.0f); }
-BB_HD float pol_gumbel(uint32_t seed, uint32_t step, uint32_t row, uint32_t i)
+// Sampling (Categorical.sample, action.py:29-33) by inverse CDF: bucket b of
+// row r draws one uniform u in [0, 1) -- word b & 1 of threefry({seed, step},
+// {r, b >> 1}) -- and takes the first action whose running sum of
+// exp(logit - max) (the terms and order of the bucket's logsumexp) exceeds
+// u * sum, the last one if rounding leaves none: 6 uniforms and no logarithm
+// per row (a Gumbel-max draw needs 19 uniforms and 38 logarithms).
+BB_HD float pol_u01(uint32_t bits) { return (float)(bits >> 8) * (1.0f / 16777216.0f); }
+BB_HD float pol_bucket_u(uint32_t seed, uint32_t step, uint32_t row, int b)
 {
     uint32_t b0, b1;
-    threefry2x32(seed, step, row, i >> 1, &b0, &b1);
-    return -pol_logf(-pol_logf(pol_u01_open((i & 1u) ? b1 : b0)));
+    threefry2x32(seed, step, row, (uint32_t)(b >> 1), &b0, &b1);
+    return pol_u01((b & 1) ? b1 : b0);
+}
+// The action of one bucket from its exp terms e[0..nb) (sum s) and uniform u.
+template <int NB>
+BB_HD int pol_inverse_cdf(const float (&e)[NB], int nb, float s, float u)
+{
+    const float t = u * s;
+    float c = 0.f;
+    int a = nb - 1;
+#pragma unroll
+    for (int i = 0; i < NB; i++) {
+        if (i < nb - 1) {
+            c = c + e[i];
+            if (a == nb - 1 && c > t) a = i;
+        }
+    }
+    return a;
 }
 
 // Bucket sampling / scoring of one row's logits (fully unrolled: the bucket
@@ -129,7 +150,7 @@ BB_HD float pol_gumbel(uint32_t seed, uint32_t step, uint32_t row, uint32_t i)
 // Logit offset of bucket b ([2, 8, 3, 2, 2, 2]).
 BB_HD constexpr int pol_bucket_off(int b) { return b == 0 ? 0 : (b == 1 ? 2 : (b == 2 ? 10 : 13 + 2 * (b - 3))); }
 
-// Bucket B of one row: its action (argmax or Gumbel-max sample) and the
+// Bucket B of one row: its action (argmax or inverse-CDF sample) and the
 // log-prob term logit[a] - logsumexp(bucket).
 template <int B>
 BB_HD void pol_bucket_term(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
@@ -139,23 +160,21 @@ BB_HD void pol_bucket_term(const float *logit, bool stochastic, uint32_t seed, u
     float mx = logit[o];
 #pragma unroll
     for (int i = 1; i < nb; i++) mx = logit[o + i] > mx ? logit[o + i] : mx;
+    float e[nb], s = 0.f;
+#pragma unroll
+    for (int i = 0; i < nb; i++) {
+        e[i] = pol_expf(logit[o + i] - mx);
+        s = s + e[i];
+    }
     int a = 0;
     if (stochastic) {
-        float best = logit[o] + pol_gumbel(seed, step, row, (uint32_t)o);
-#pragma unroll
-        for (int i = 1; i < nb; i++) {
-            const float g = logit[o + i] + pol_gumbel(seed, step, row, (uint32_t)(o + i));
-            if (g > best) { best = g; a = i; }
-        }
+        a = pol_inverse_cdf(e, nb, s, pol_bucket_u(seed, step, row, B));
     } else {
         float best = logit[o];
 #pragma unroll
         for (int i = 1; i < nb; i++)
             if (logit[o + i] > best) { best = logit[o + i]; a = i; }  // first maximum (torch argmax)
     }
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < nb; i++) s = s + pol_expf(logit[o + i] - mx);
     const float lse = mx + pol_logf(s);
     float la = logit[o];
 #pragma unroll

@@ -1,6 +1,6 @@
 // bb_policy.hip -- fused policy inference on gfx950:
 // observation rows -> RunningMeanStd -> 2 x (Linear + LayerNorm + ReLU) ->
-// actor/critic heads -> per-bucket argmax or Gumbel-max sample, log-prob and
+// actor/critic heads -> per-bucket argmax or categorical sample, log-prob and
 // value, written straight into the simulator's action tensor (bb_policy.h has
 // the row math and the reference lines).
 //
@@ -524,7 +524,7 @@ inline PolicyWgGrid policy_wg_grid(int64_t tiles)
 }
 
 // M-tiles per wave.  4: 64 rows per wave, one row per lane in the bucket
-// pass, each lane's 19 Gumbel draws in series; 1: 16 rows per wave, 4 lanes
+// pass, each lane's buckets in series; 1: 16 rows per wave, 4 lanes
 // per row in the bucket pass.  Measured (profiles/r03/e_policy_mt_ab.txt):
 // 8 192 rows 18.1 (MT 4) -> 13.9-18.6 us (MT 1), 65 536 rows 24.8 (MT 4) vs
 // 28.8 us (MT 1): MT = 1 below POLICY_MT4_ROWS rows.  MADRONA_BB_POLICY_MT

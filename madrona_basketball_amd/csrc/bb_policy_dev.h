@@ -69,10 +69,10 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
 
 // Bucket pass of R < 64 rows: LPR = 64 / R lanes per row,
 // every step the same instructions on different data (no divergent roles):
-//   A  lane part p: the Gumbel noise of logit pairs p, p + LPR, ... (one
-//      threefry call per pair) and, per logit, g = logit + noise and
-//      e = exp(logit - bucket max), into LDS;
-//   B  lane part p: buckets p, p + LPR, ...: first maximum of g, sum of e in
+//   A  lane part p: e = exp(logit - bucket max) of logits p, p + LPR, ...,
+//      into LDS;
+//   B  lane part p: buckets p, p + LPR, ...: the action (first maximum, or
+//      the inverse-CDF draw over the bucket's e in logit order), sum of e in
 //      logit order, logit - logsumexp, into LDS;
 //   C  lane part 0: the six terms summed in bucket order, the outputs.
 // Every value is the one pol_bucket_term / pol_select computes (same
@@ -80,17 +80,17 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
 // The bucket pass's LDS exchange of one wave (R rows).
 template <int R>
 struct BucketLds {
-    float g[R][POL_LOGITS + 1], e[R][POL_LOGITS + 1], t[R][POL_BUCKETS];
+    float e[R][POL_LOGITS + 1], t[R][POL_BUCKETS];
     int32_t a[R][POL_BUCKETS];
 };
 
-// The Gumbel noise a lane of the R-row bucket pass uses: logits 2 pr + h of
-// its pairs pr = part + LPR j (pol_gumbel's values).  It depends only on
-// (seed, step, row, logit), so a caller may compute it ahead of the logits.
+// The uniforms a lane of the R-row bucket pass draws: buckets part + LPR j
+// (pol_bucket_u's values).  They depend only on (seed, step, row, bucket), so
+// a caller may draw them ahead of the logits.
 template <int R>
 struct BucketNoise {
-    static constexpr int LPR = 64 / R, PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR;
-    float g[PPL][2];
+    static constexpr int LPR = 64 / R, BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    float u[BPL];
 };
 template <int R>
 __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, uint32_t step, int64_t row0, int64_t rows,
@@ -100,18 +100,15 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
     const int r = lane / BN::LPR, part = lane % BN::LPR;
     const int64_t rr = row0 + r;
 #pragma unroll
-    for (int j = 0; j < BN::PPL; j++) {
-        const int pr = part + BN::LPR * j;
-        uint32_t b0 = 0, b1 = 0;
-        if (pr < BN::PAIRS && rr < rows) threefry2x32(seed, step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
-#pragma unroll
-        for (int h = 0; h < 2; h++) n.g[j][h] = -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
+    for (int j = 0; j < BN::BPL; j++) {
+        const int b = part + BN::LPR * j;
+        n.u[j] = (b < POL_BUCKETS && rr < rows) ? pol_bucket_u(seed, step, (uint32_t)rr, b) : 0.f;
     }
 }
 
 // R rows (8, 16 or 32) over the wave's 64 lanes.  act_local (optional): row
 // r's six actions also into act_local[r] (LDS).  pre (optional): this
-// lane's noise, computed ahead by bucket_noise with a's seed and step.
+// lane's uniforms, drawn ahead by bucket_noise with a's seed and step.
 // ts (diagnostics, optional): lane 0 writes the clock after the maxima, the
 // per-logit part, the per-bucket part and the outputs into ts[0..3].
 __device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
@@ -121,8 +118,8 @@ __device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
         if (lane == 0) ts[i] = c;
     }
 }
-// PRE (compile-time, so that the noise stays in registers: a runtime-null
-// pointer to it would put it in scratch): `pre` holds this lane's noise.
+// PRE (compile-time, so that the uniforms stay in registers: a runtime-null
+// pointer to them would put them in scratch): `pre` holds this lane's draws.
 // STOCH: -1 a.stochastic at run time, 0 / 1 fixed at compile time.
 template <int R, bool PRE = false, int STOCH = -1>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
@@ -131,8 +128,8 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
 {
     static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
     constexpr int LPR = 64 / R;
-    constexpr int PAIRS = (POL_LOGITS + 1) / 2, PPL = (PAIRS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
-    float (*gbuf)[POL_LOGITS + 1] = buf.g, (*ebuf)[POL_LOGITS + 1] = buf.e, (*tbuf)[POL_BUCKETS] = buf.t;
+    constexpr int LGL = (POL_LOGITS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    float (*ebuf)[POL_LOGITS + 1] = buf.e, (*tbuf)[POL_BUCKETS] = buf.t;
     int32_t (*abuf)[POL_BUCKETS] = buf.a;
     const int r = lane / LPR, part = lane % LPR;
     const int64_t rr = row0 + r;
@@ -151,29 +148,14 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     if (ts) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (diagnostics)
     bucket_stamp(ts, 0, lane);
 #pragma unroll
-    for (int j = 0; j < PPL; j++) {
-        const int pr = part + LPR * j;
-        if (pr < PAIRS) {
-            uint32_t b0 = 0, b1 = 0;
-            if (!PRE && stochastic && live) threefry2x32(a.seed, a.step, (uint32_t)rr, (uint32_t)pr, &b0, &b1);
+    for (int j = 0; j < LGL; j++) {
+        const int i = part + LPR * j;
+        if (i < POL_LOGITS) {
+            const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
+            float m = mx[0];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                const int i = 2 * pr + h;
-                if (i < POL_LOGITS) {
-                    const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
-                    float m = mx[0];
-#pragma unroll
-                    for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
-                    const float x = lg[i];
-                    // pol_gumbel's value for logit i (its threefry word h)
-                    float nz;
-                    if constexpr (PRE) nz = pre->g[j][h];
-                    else nz = -pol_logf(-pol_logf(pol_u01_open(h ? b1 : b0)));
-                    const float g = stochastic ? x + nz : x;
-                    gbuf[r][i] = g;
-                    ebuf[r][i] = pol_expf(x - m);
-                }
-            }
+            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
+            ebuf[r][i] = pol_expf(lg[i] - m);
         }
     }
     pol_wave_sync();
@@ -183,14 +165,30 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         const int b = part + LPR * j;
         if (b < POL_BUCKETS) {
             const int o = pol_bucket_off(b), nb = pol_bucket(b);
-            float best = gbuf[r][o], s = ebuf[r][o];
-            int act = 0;
+            float e[8];
+            e[0] = ebuf[r][o];
+            float s = e[0];
 #pragma unroll
             for (int i = 1; i < 8; i++) {
                 if (i < nb) {
-                    const float g = gbuf[r][o + i];
-                    if (g > best) { best = g; act = i; }  // first maximum
-                    s = s + ebuf[r][o + i];
+                    e[i] = ebuf[r][o + i];
+                    s = s + e[i];
+                }
+            }
+            int act = 0;
+            if (stochastic) {
+                float u;
+                if constexpr (PRE) u = pre->u[j];
+                else u = live ? pol_bucket_u(a.seed, a.step, (uint32_t)rr, b) : 0.f;
+                act = pol_inverse_cdf(e, nb, s, u);
+            } else {
+                float best = lg[o];
+#pragma unroll
+                for (int i = 1; i < 8; i++) {
+                    if (i < nb) {
+                        const float g = lg[o + i];
+                        if (g > best) { best = g; act = i; }  // first maximum
+                    }
                 }
             }
             float m = mx[0];

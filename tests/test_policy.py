@@ -7,7 +7,7 @@ structure.  Bars: host executor == gfx950 kernel bit for bit (same arithmetic
 order, bb_policy.h); both vs the torch restatement within fp32 tolerance
 (value / log-prob |diff| <= 2e-5 + 2e-5 |x|, written in the test), argmax
 actions equal wherever the top two logits of a bucket are > 1e-4 apart;
-Gumbel-max samples follow softmax(logits) (binomial 5-sigma bounds).
+inverse-CDF samples follow softmax(logits) (binomial 5-sigma bounds).
 """
 import numpy as np
 import pytest
@@ -119,7 +119,7 @@ def test_host_policy_act_writes_one_agent_column(native_lib):
     assert torch.all((after[:, 1] >= 0) & (after[:, 1] < hi))
 
 
-def test_host_policy_gumbel_sampling_follows_softmax(native_lib):
+def test_host_policy_sampling_follows_softmax(native_lib):
     """20 000 copies of one observation row: per-bucket sample frequencies
     match softmax(logits) within 5 binomial sigma; log-probs are those of the
     sampled actions."""

@@ -85,7 +85,7 @@ def test_host_policy_matches_reference_agent(native_lib, case):
 
 @pytest.mark.parametrize("case", CASES)
 def test_host_policy_sampled_logprob_matches_reference_logits(native_lib, case):
-    """Gumbel-max samples: their log-probs are the reference's log-softmax at
+    """Sampled actions (inverse CDF): their log-probs are the reference's log-softmax at
     the sampled actions."""
     obs, sd, ref = load_case(case)
     pol = FusedPolicy.from_agent(agent_from_state_dict(sd))
