@@ -1010,10 +1010,24 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             (void)hipFree(ts);
         }
     }
+    // buffer.obs[k + 1] (the trainee's rows after step k) is written by step
+    // k's row passes as whole-line stores (Params::rec_obs), so policy pass
+    // k >= 1 reads its rows without recording them: from the policy's
+    // registers the record took 9 us of a 61.6 us step at 65 536 worlds
+    // (each store instruction touching 64 rows' lines; profiles/r04/h_*)
     for (int32_t k = 0; k < (fused ? 0 : n); k++) {
-        hipError_t e = bb::launch_policy(pass(k, false), st);
+        bb::PolicyArgs a = pass(k, false);
+        if (k > 0) a.obs_out = nullptr;
+        hipError_t e = bb::launch_policy(a, st);
         if (e == hipSuccess && opponent) e = bb::launch_policy(opp_pass(k), st);
-        if (e == hipSuccess) e = bb::launch_step(s->n, s->p, st);
+        if (e == hipSuccess) {
+            bb::Params p = s->p;
+            if (out->obs && k + 1 < n) {
+                p.rec_obs = out->obs + (int64_t)(k + 1) * W * bb::POL_IN;
+                p.rec_agent = trainee;
+            }
+            e = bb::launch_step(s->n, p, st);
+        }
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
     }
     if (final_needed && !fused) {

@@ -354,8 +354,19 @@ __device__ __forceinline__ void row_store(char *base, uint32_t off, vf4 v)
     }
 }
 
+// The record of agent `agent`'s rows (Params::rec_obs, N = 2): row r of the
+// wave's tile (world r / N, agent r % N) also goes to base + (r / N) * 512
+// (+ the pass's piece offset); base == nullptr: no record.
+struct RecRows {
+    char *base;
+    int agent;
+};
+#ifndef BB_REC_AUX
+#define BB_REC_AUX 2  // record rows: non-temporal (a fresh [K][W][128] buffer, beyond the cache for K >= 8)
+#endif
+
 template <int N, int QT, int RS, int Q0, int QN, int RSTR, bool ALL, int QZ, int AUX>
-__device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64_t staged, int lane)
+__device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64_t staged, int lane, RecRows rec)
 {
     // pieces q >= QZ of this pass are zeros (row padding), not read from the tile
     constexpr int OW = obs_width(N);
@@ -365,13 +376,15 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
 #pragma unroll
     for (int b0 = 0; b0 < QT; b0 += BS) {
         vf4 v[BS];
-        uint32_t go[BS];
-        bool ok[BS];
+        uint32_t go[BS], ro[BS];
+        bool ok[BS], rk[BS];
 #pragma unroll
         for (int j = 0; j < BS; j++) {
             if (b0 + j < QT) {
                 ok[j] = (QN == QT || q < QN) && (ALL || ((staged >> r) & 1ull));
                 go[j] = (uint32_t)(r * (RSTR * OW * 4) + q * 16);
+                rk[j] = ok[j] && (r % N) == rec.agent;
+                ro[j] = (uint32_t)((r / N) * (OW * 4) + q * 16);
                 if (ok[j]) {
                     v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
                     if (QZ < QN && q >= QZ) v[j] = vf4{0.f, 0.f, 0.f, 0.f};
@@ -384,15 +397,22 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
 #pragma unroll
         for (int j = 0; j < BS; j++)
             if (b0 + j < QT && ok[j]) row_store<AUX>(base, go[j], v[j]);
+        if (rec.base) {  // wave-uniform
+#pragma unroll
+            for (int j = 0; j < BS; j++)
+                if (b0 + j < QT && rk[j]) row_store<BB_REC_AUX>(rec.base, ro[j], v[j]);
+        }
     }
 }
 
 template <int N, int QT, int RS, int Q0, int QN, int RSTR, int QZ = QN, int AUX = -1>
-__device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane)
+__device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane,
+                                           RecRows rec = RecRows{nullptr, 0})
 {
     char *base = (char *)(obs + row0 * obs_width(N) + 4 * Q0);  // wave-uniform
-    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true, QZ, AUX>(tile, base, staged, lane);
-    else flush_rows<N, QT, RS, Q0, QN, RSTR, false, QZ, AUX>(tile, base, staged, lane);
+    if (rec.base) rec.base += 16 * Q0;
+    if (staged == ~0ull) flush_rows<N, QT, RS, Q0, QN, RSTR, true, QZ, AUX>(tile, base, staged, lane, rec);
+    else flush_rows<N, QT, RS, Q0, QN, RSTR, false, QZ, AUX>(tile, base, staged, lane, rec);
 }
 
 struct Intrinsic {
@@ -413,16 +433,17 @@ __device__ __forceinline__ void emit_phase(const World<N> &v, const Ctx &c, cons
 
 template <int N, int MODE, class T, int PHASE = 0>
 __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
-                                           bool fast, float *tile, float *obs, int64_t row0, int lane, int32_t ib)
+                                           bool fast, float *tile, float *obs, int64_t row0, int lane, int32_t ib,
+                                           RecRows rec = RecRows{nullptr, 0})
 {
     if (fast) emit_phase<N, T, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     __syncthreads();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
     constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
-    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, row0, __ballot(fast), lane);
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, row0, __ballot(fast), lane, rec);
     if constexpr (PHASE + 1 < T::PH) {
         __syncthreads();
-        obs_phases<N, MODE, T, PHASE + 1>(v, c, sh, share, fast, tile, obs, row0, lane, ib);
+        obs_phases<N, MODE, T, PHASE + 1>(v, c, sh, share, fast, tile, obs, row0, lane, ib, rec);
     }
 }
 
@@ -494,7 +515,7 @@ __device__ __forceinline__ void lane_shared_obs(const World<N> &v, const Ctx &c,
     }
 }
 
-template <int N, int MODE, class T = PhasedTile<N>>
+template <int N, int MODE, class T = PhasedTile<N>, bool REC = false>
 __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
                                                int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
 {
@@ -516,13 +537,32 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
             }
         }
     } else {
-        if (active && !fast) fill_obs_slow(v, c, 0, grow, ib);
-        obs_phases<N, MODE, T>(v, c, sh, share, fast, tile, obs, w0 * N, lane, ib);
+        // PPO's buffer.obs record of agent rec_agent (Params::rec_obs, N = 2)
+        RecRows rec{nullptr, 0};
+        if constexpr (REC) rec = RecRows{(char *)(c.p->rec_obs + w0 * (int64_t)OW), c.p->rec_agent};
+        if (active && !fast) {
+            fill_obs_slow(v, c, 0, grow, ib);
+            if (rec.base && k == rec.agent) fill_obs_slow(v, c, 0, c.p->rec_obs + w * (int64_t)OW, ib);
+        }
+        obs_phases<N, MODE, T>(v, c, sh, share, fast, tile, obs, w0 * N, lane, ib, rec);
+        if (REC && T::QW < OW / 4) {
+            // the record rows' zero tail (pieces QW .. OW/4 - 1), which the
+            // passes do not write (the sim's own rows keep theirs from construction)
+            constexpr int ZP = OW / 4 - T::QW, TOT = (WAVE / N) * ZP;
+            const vf4 z = {0.f, 0.f, 0.f, 0.f};
+            const uint64_t staged = __ballot(fast);  // rows that went through the tile
+#pragma unroll
+            for (int i = 0; i < (TOT + WAVE - 1) / WAVE; i++) {
+                const int f = i * WAVE + lane, wl = f / ZP;
+                if (f < TOT && ((staged >> (wl * N + rec.agent)) & 1ull))
+                    row_store<BB_REC_AUX>(rec.base, (uint32_t)(wl * OW * 4 + (T::QW + f % ZP) * 16), z);
+            }
+        }
     }
 }
 
 // One lane per agent: lane = (w - w0) * N + k.
-template <int N, int MODE, bool LINES>
+template <int N, int MODE, bool LINES, bool REC = false>
 __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 {
     using T = StepTile<N, LINES>;
@@ -576,7 +616,7 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 
     const int32_t ib = active ? inbounder_id(s) : -1;
     const bool share = active && obs_sharable(s);
-    agent_lane_obs<N, MODE, T>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
+    agent_lane_obs<N, MODE, T, REC>(v, c, ib, share, k, lane, w0, w, active, tile, p.c.obs);
     trace_point<MODE>(p, 9);
 }
 
@@ -1758,7 +1798,10 @@ __device__ __forceinline__ void start_skew()
 #ifndef BB_STEP_MINW
 #define BB_STEP_MINW 2  // waves per SIMD the register budget is sized for
 #endif
-template <int N, int MODE, bool LINES = false>
+// REC: the step also records agent rec_agent's rows into Params::rec_obs
+// (PPO's per-step loop, N = 2; a separate instantiation, so the plain step
+// carries none of it)
+template <int N, int MODE, bool LINES = false, bool REC = false>
 __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
 {
     __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
@@ -1772,7 +1815,7 @@ __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
         }
         step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm);
     } else if constexpr (Lanes<N>::LPW == N) {
-        step_agent_lanes<N, MODE, LINES>(p, (float *)tile4);
+        step_agent_lanes<N, MODE, LINES, REC>(p, (float *)tile4);
     } else {
         step_world_lanes<N, MODE>(p, (float *)tile4);
     }
@@ -1829,6 +1872,13 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
     constexpr int WPB = Lanes<N>::WPB;
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
+    if constexpr (Lanes<N>::LPW == N && !Lanes<N>::SHARED) {
+        if (mode == MODE_FULL && p.rec_obs) {
+            if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL((k_step<N, MODE_FULL, true, true>), grid, block, 0, s, ev0, ev1, 0, p);
+            else hipExtLaunchKernelGGL((k_step<N, MODE_FULL, false, true>), grid, block, 0, s, ev0, ev1, 0, p);
+            return hipGetLastError();
+        }
+    }
     switch (mode) {
     case MODE_FULL:
         if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL(k_step<N, MODE_FULL, true>, grid, block, 0, s, ev0, ev1, 0, p);

@@ -292,7 +292,7 @@ __global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a
             }
             __builtin_amdgcn_sched_barrier(0);
         }
-        ln_relu_to_tile(a0, a1, cs[0][c], cs[0][c + 16], cs[1][c], cs[1][c + 16], cs[2][c], cs[2][c + 16], tile, c, q);
+        ln_relu_to_tile<false>(a0, a1, cs[0][c], cs[0][c + 16], cs[1][c], cs[1][c + 16], cs[2][c], cs[2][c + 16], tile, c, q);
         pol_wave_sync();
         // layer 2, then the heads (k = 8q + j)
 #pragma unroll
@@ -318,7 +318,7 @@ __global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a
                 a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w1[j], a1, 0, 0, 0);
             }
             if (layer == 0) {
-                ln_relu_to_tile(a0, a1, cs[3][c], cs[3][c + 16], cs[4][c], cs[4][c + 16], cs[5][c], cs[5][c + 16], tile, c, q);
+                ln_relu_to_tile<false>(a0, a1, cs[3][c], cs[3][c + 16], cs[4][c], cs[4][c + 16], cs[5][c], cs[5][c + 16], tile, c, q);
             } else {
 #pragma unroll
                 for (int i = 0; i < 4; i++) {

@@ -50,20 +50,65 @@ __device__ __forceinline__ float quarter_sum(float t)
     return t;
 }
 
+// 1 / sqrt(var[i] + eps) of the 4 rows a lane holds: every lane of a 16-lane
+// row group holds the same four variances, so lane c evaluates only row
+// (c & 3)'s (the correctly rounded square root and quotient are ~25
+// instructions) and the quad's lanes exchange them by DPP broadcasts.  The
+// values are the ones each lane would compute itself.
+__device__ __forceinline__ void ln_inv4(const float (&var)[4], int c, float (&inv)[4])
+{
+    // var[c & 3] by bit masks behind an empty asm: as a select chain the
+    // compiler turned it into an indexed private array (a scratch round trip)
+    uint32_t me = (uint32_t)(c & 3);
+    __asm__ volatile("" : "+v"(me));
+    uint32_t v = __builtin_bit_cast(uint32_t, var[0]);
+#pragma unroll
+    for (int i = 1; i < 4; i++) {
+        const uint32_t m = 0u - (uint32_t)(me == (uint32_t)i);
+        v = (v & ~m) | (__builtin_bit_cast(uint32_t, var[i]) & m);
+    }
+    const float mine = 1.0f / bbm::sqrtf_(__builtin_bit_cast(float, v) + 1e-5f);
+    inv[0] = dpp_f<0x00>(mine);  // quad_perm [0,0,0,0]
+    inv[1] = dpp_f<0x55>(mine);  // [1,1,1,1]
+    inv[2] = dpp_f<0xAA>(mine);  // [2,2,2,2]
+    inv[3] = dpp_f<0xFF>(mine);  // [3,3,3,3]
+}
+
 // LayerNorm + ReLU of the 4 rows a lane holds (cols c and c + 16), then the
-// result into the LDS tile [row][col].
+// result into the LDS tile [row][col].  SPREAD: the inverse deviations by
+// ln_inv4 (k_policy: 25.3 -> 25.2 us at 65 536 rows); k_policy_wg keeps one
+// per lane and row (with ln_inv4 it measured 28.0 -> 51.6 us, profiles/r04/k_*).
+template <bool SPREAD = true>
 __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0, float bias1, float w0, float w1,
                                                 float lb0, float lb1, float (*tile)[33], int c, int q)
 {
+    if constexpr (SPREAD) {
+        float d0[4], d1[4], var[4], inv[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
-        const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
-        const float d0 = h0 - mean, d1 = h1 - mean;
-        const float var = quarter_sum((d0 * d0) + (d1 * d1)) * (1.0f / 32.0f);
-        const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
-        tile[4 * q + i][c] = pol_relu(((d0 * inv) * w0) + lb0);
-        tile[4 * q + i][c + 16] = pol_relu(((d1 * inv) * w1) + lb1);
+        for (int i = 0; i < 4; i++) {
+            const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
+            const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
+            d0[i] = h0 - mean;
+            d1[i] = h1 - mean;
+            var[i] = quarter_sum((d0[i] * d0[i]) + (d1[i] * d1[i])) * (1.0f / 32.0f);
+        }
+        ln_inv4(var, c, inv);
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            tile[4 * q + i][c] = pol_relu(((d0[i] * inv[i]) * w0) + lb0);
+            tile[4 * q + i][c + 16] = pol_relu(((d1[i] * inv[i]) * w1) + lb1);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const float h0 = a0[i] + bias0, h1 = a1[i] + bias1;
+            const float mean = quarter_sum(h0 + h1) * (1.0f / 32.0f);
+            const float d0 = h0 - mean, d1 = h1 - mean;
+            const float var = quarter_sum((d0 * d0) + (d1 * d1)) * (1.0f / 32.0f);
+            const float inv = 1.0f / bbm::sqrtf_(var + 1e-5f);
+            tile[4 * q + i][c] = pol_relu(((d0 * inv) * w0) + lb0);
+            tile[4 * q + i][c + 16] = pol_relu(((d1 * inv) * w1) + lb1);
+        }
     }
 }
 
@@ -136,6 +181,12 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     const bool live = rr < a.rows;
     const bool stochastic = STOCH < 0 ? a.stochastic != 0 : STOCH == 1;
     const float *lg = tile[r];
+    // this lane's uniforms, drawn before the LDS work (in pass B the threefry
+    // chain raised k_policy_wg over its register budget)
+    BucketNoise<R> own;
+    if constexpr (!PRE) {
+        if (stochastic) bucket_noise<R>(own, a.seed, a.step, row0, a.rows, lane);
+    }
     // bucket maxima (every lane, compile-time indices)
     float mx[POL_BUCKETS];
 #pragma unroll
@@ -165,22 +216,25 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
         const int b = part + LPR * j;
         if (b < POL_BUCKETS) {
             const int o = pol_bucket_off(b), nb = pol_bucket(b);
-            float e[8];
-            e[0] = ebuf[r][o];
-            float s = e[0];
+            float s = ebuf[r][o];
 #pragma unroll
-            for (int i = 1; i < 8; i++) {
-                if (i < nb) {
-                    e[i] = ebuf[r][o + i];
-                    s = s + e[i];
-                }
-            }
+            for (int i = 1; i < 8; i++)
+                if (i < nb) s = s + ebuf[r][o + i];
             int act = 0;
             if (stochastic) {
-                float u;
-                if constexpr (PRE) u = pre->u[j];
-                else u = live ? pol_bucket_u(a.seed, a.step, (uint32_t)rr, b) : 0.f;
-                act = pol_inverse_cdf(e, nb, s, u);
+                // pol_inverse_cdf over the bucket's terms, read again from LDS
+                // (the same running sums: no register copy of the terms)
+                const float u = PRE ? pre->u[j] : own.u[j];
+                const float t = u * s;
+                float cs = 0.f;
+                act = nb - 1;
+#pragma unroll
+                for (int i = 0; i < 7; i++) {
+                    if (i < nb - 1) {
+                        cs = cs + ebuf[r][o + i];
+                        if (act == nb - 1 && cs > t) act = i;
+                    }
+                }
             } else {
                 float best = lg[o];
 #pragma unroll

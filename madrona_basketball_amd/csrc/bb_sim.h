@@ -337,6 +337,11 @@ struct Params {
     uint32_t diag_dup;           // diagnostics only (MODE_SKIP): systems to run twice
     uint32_t diag_keep;          // diagnostics only: 0 (the duplicate run's result is dropped)
     uint64_t *diag_ts;           // diagnostics only (MODE_TRACE): TRACE_POINTS clocks per wave
+    // PPO's buffer.obs record (bb_rollout_policy, scripts/ppo.py:129; N = 2):
+    // when set, the step also writes agent rec_agent's observation row of
+    // world w to rec_obs + w * 128 (the whole 128 floats, zero tail included)
+    float *rec_obs;
+    int32_t rec_agent;
 };
 
 BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
