@@ -331,12 +331,17 @@ __device__ __forceinline__ void policy_layers(float (&x)[MT][32], const PolicyRe
         nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
         ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
     }
+    // Software-pipelined over the M-tiles: the MFMA chain of tile m is issued
+    // before the VALU work of tile m - 1 (its LayerNorm) and of tile m + 1
+    // (its normalisation), which then run while the matrix pipe works
+    // through tile m.  Blocks fenced by scheduling barriers, so each keeps its
+    // place: the normalisation as one block, then the MFMA chain back to back
+    // (interleaved, every MFMA waits out a VALU-write hazard).
+    f32x4 acc[MT][2];
+#pragma unroll
+    for (int j = 0; j < 32; j++) x[0][j] = pol_clamp((x[0][j] - nm[j]) * ni[j]);
 #pragma unroll
     for (int m = 0; m < MT; m++) {
-        // the VALU normalisation as one block, then the MFMA chain back to back
-        // (interleaved, every MFMA waits out a VALU-write hazard)
-#pragma unroll
-        for (int j = 0; j < 32; j++) x[m][j] = pol_clamp((x[m][j] - nm[j]) * ni[j]);
         __builtin_amdgcn_sched_barrier(0);
         f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -344,9 +349,22 @@ __device__ __forceinline__ void policy_layers(float (&x)[MT][32], const PolicyRe
             a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], R.w1[0][j], a0, 0, 0, 0);
             a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[m][j], R.w1[1][j], a1, 0, 0, 0);
         }
+        acc[m][0] = a0;
+        acc[m][1] = a1;
         __builtin_amdgcn_sched_barrier(0);
-        ln_relu_to_tile(a0, a1, R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1, tile + 16 * m, c, q);
+        if (m + 1 < MT) {
+#pragma unroll
+            for (int j = 0; j < 32; j++) x[m + 1][j] = pol_clamp((x[m + 1][j] - nm[j]) * ni[j]);
+        }
+        if (m > 0) {
+            __builtin_amdgcn_sched_barrier(0);
+            ln_relu_to_tile(acc[m - 1][0], acc[m - 1][1], R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1,
+                            tile + 16 * (m - 1), c, q);
+        }
     }
+    __builtin_amdgcn_sched_barrier(0);
+    ln_relu_to_tile(acc[MT - 1][0], acc[MT - 1][1], R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1,
+                    tile + 16 * (MT - 1), c, q);
     pol_wave_sync();
     // layer 2 and heads, per M-tile through its 16 rows of the tile
 #pragma unroll

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round 4, session m: layer-1 software pipeline over M-tiles (parity + timing).
+set -u
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R"
+OUT=gpurun_out/m
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python3 -u -m pytest tests/test_policy_rollout.py tests/test_policy.py tests/test_policy_wg.py \
+    tests/test_policy_golden.py -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+rc=$?; tail -3 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do
+timeout -k 10 120 python3 tools/policy_time.py --worlds 65536 2>&1 | grep -v amdgpu.ids | grep "agent 0" | sed "s|^|MT4 |" || exit 1
+done
+timeout -k 10 120 python3 tools/policy_time.py --worlds 65536 --trace --only-argmax 2>&1 | grep -v amdgpu.ids | sed "s|^|MT4 |" || exit 1
+timeout -k 10 300 python3 tools/ppo_time.py --worlds 65536 --rollouts 4 2>&1 | grep -v amdgpu.ids | grep "all records" || exit 1
