@@ -259,6 +259,10 @@ struct bb_sim {
     void *slot[NUM_SLOTS] = {};
     bb::Params p;
     std::unique_ptr<bb::HostPool> pool;  // ExecMode.CPU workers (created with the simulator)
+    // (CUDA mode) the second stream and events of bb_rollout_policy's split
+    // per-step loop, created on first use
+    hipStream_t aux = nullptr;
+    hipEvent_t aux_ev[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -570,6 +574,13 @@ int bb_create_with_buffers(const bb_config *cfg, void *const *bufs, int32_t nbuf
 int bb_destroy(bb_sim *s)
 {
     if (!s) return BB_OK;
+    if (s->aux) {
+        DeviceGuard g(s->device);
+        (void)hipStreamSynchronize(s->aux);
+        for (hipEvent_t e : s->aux_ev)
+            if (e) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(s->aux);
+    }
     if (s->owns) {
         for (int id = 0; id < NUM_SLOTS; id++) {
             if (!s->slot[id]) continue;
@@ -883,6 +894,46 @@ bb::PolicyWeights policy_weights(const bb_policy_weights *w)
 
 }  // namespace
 
+// Params of worlds [w0, w0 + count) of a simulator: every column advanced by
+// w0 worlds, world_offset (the per-world RNG key) too, so the part steps
+// exactly as those worlds of the whole (the worlds are independent).
+bb::Params shard_params(const bb::Params &p, int N, int64_t w0, int64_t count)
+{
+    bb::Params q = p;
+    bb::Columns &c = q.c;
+    const auto off = [&](auto *&ptr, int64_t per_world) {
+        if (ptr) ptr += w0 * per_world;
+    };
+    off(c.reset, N); off(c.game_state, 14); off(c.action, N * 6); off(c.action_mask, N * 4);
+    off(c.agent_pos, N * 3); off(c.obs, N * bb::obs_width(N)); off(c.reward, N); off(c.done, N);
+    off(c.agent_id, N); off(c.possession, N * 3); off(c.orientation, N * 4); off(c.team, N * 5);
+    off(c.stats, N * 2); off(c.ball_pos, 3); off(c.ball_physics, 7); off(c.ball_id, 1); off(c.ball_grabbed, 2);
+    off(c.ball_vel, 3); off(c.hoop_pos, 6); off(c.agent_vel, N * 3); off(c.cooldown, N); off(c.cur_step, N);
+    off(c.inbounding, N * 2); off(c.attributes, N * 10); off(c.world_clock, 1); off(c.rng_counter, 1);
+    q.num_worlds = count;
+    q.world_offset = p.world_offset + w0;
+    return q;
+}
+
+// Split per-step PPO loop (bb_rollout_policy) from this many worlds on: the
+// two halves of the worlds run on two streams, half B's policy pass k after
+// half A's, so one half's policy pass (latency-bound) runs beside the other
+// half's step (memory-bound).  The halves' policy passes take k_policy<1>
+// (124 VGPRs: a policy wave and a step wave share a SIMD; k_policy<4>'s 240
+// do not, and then the kernels only alternate: 58.9 us per step at 65 536
+// worlds).  Measured per step, K = 32, all records (profiles/r04/r_*):
+// 32 768 worlds 41.0 -> 37.5-38.5 us, 65 536 56.1 -> 54.3-55.6, 131 072
+// 99.5 -> 92.5, 262 144 187.2 -> 176.4.  MADRONA_BB_PPO_SPLIT_MIN_WORLDS
+// overrides it (0: never split).
+static int64_t ppo_split_min_worlds()
+{
+    static const int64_t v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_MIN_WORLDS");
+        return (int64_t)(e && *e ? std::atoll(e) : 32768);
+    }();
+    return v;
+}
+
 // The fused PPO rollout (k_rollout_policy) runs one workgroup of 3 waves per
 // 32 worlds at one workgroup per CU (register-bound): used up to two waves of
 // workgroups -- measured 8 192 worlds 15.1 vs 27.6 us per step unfused,
@@ -1010,25 +1061,86 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             (void)hipFree(ts);
         }
     }
+    // one part (worlds [w0, w0 + cnt)) of policy pass k (or of the opponent's)
+    const auto part_pass = [&](bb::PolicyArgs a, int64_t w0, int64_t cnt, const bb::Params &sp) {
+        const auto adv = [&](auto *&ptr, int64_t per) {
+            if (ptr) ptr += w0 * per;
+        };
+        a.obs += w0 * N * ow;
+        a.rows = cnt;
+        adv(a.actions, N * 6);
+        adv(a.obs_out, bb::POL_IN);
+        adv(a.act_out, 6);
+        adv(a.log_prob, 1);
+        adv(a.value, 1);
+        if (a.rew_src) {
+            a.rew_src = sp.c.reward + (a.rew_src - c.reward);
+            a.done_src = sp.c.done + (a.done_src - c.done);
+            adv(a.rew_out, 1);
+            adv(a.done_out, 1);
+        }
+        a.key_row0 = (uint32_t)w0;
+        a.mt = 1;  // 124 VGPRs: a policy wave fits beside a step wave on one SIMD
+        return a;
+    };
+    const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
+    const int parts = split ? 2 : 1;
+    const int64_t half = (W + 1) / 2;
+    hipStream_t pst[2] = {st, st};
+    if (split) {
+        if (!s->aux) {
+            if (hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking) != hipSuccess) return fail(BB_ERR_HIP, "hipStreamCreate");
+            for (hipEvent_t &e : s->aux_ev)
+                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(BB_ERR_HIP, "hipEventCreate");
+        }
+        pst[1] = s->aux;
+        (void)hipEventRecord(s->aux_ev[0], st);  // part B starts after everything before the call
+        (void)hipStreamWaitEvent(s->aux, s->aux_ev[0], 0);
+    }
+    bb::Params sp[2];
+    int64_t pw0[2], pcnt[2];
+    for (int h = 0; h < parts; h++) {
+        pw0[h] = split ? h * half : 0;
+        pcnt[h] = split ? (h == 0 ? half : W - half) : W;
+        sp[h] = split ? shard_params(s->p, s->n, pw0[h], pcnt[h]) : s->p;
+    }
     // buffer.obs[k + 1] (the trainee's rows after step k) is written by step
     // k's row passes as whole-line stores (Params::rec_obs), so policy pass
     // k >= 1 reads its rows without recording them: from the policy's
     // registers the record took 9 us of a 61.6 us step at 65 536 worlds
     // (each store instruction touching 64 rows' lines; profiles/r04/h_*)
     for (int32_t k = 0; k < (fused ? 0 : n); k++) {
-        bb::PolicyArgs a = pass(k, false);
-        if (k > 0) a.obs_out = nullptr;
-        hipError_t e = bb::launch_policy(a, st);
-        if (e == hipSuccess && opponent) e = bb::launch_policy(opp_pass(k), st);
-        if (e == hipSuccess) {
-            bb::Params p = s->p;
-            if (out->obs && k + 1 < n) {
-                p.rec_obs = out->obs + (int64_t)(k + 1) * W * bb::POL_IN;
-                p.rec_agent = trainee;
+        for (int h = 0; h < parts; h++) {
+            bb::PolicyArgs a = pass(k, false);
+            if (k > 0) a.obs_out = nullptr;
+            if (split) a = part_pass(a, pw0[h], pcnt[h], sp[h]);
+            hipError_t e = bb::launch_policy(a, pst[h]);
+            if (e == hipSuccess && opponent) {
+                bb::PolicyArgs o = opp_pass(k);
+                if (split) o = part_pass(o, pw0[h], pcnt[h], sp[h]);
+                e = bb::launch_policy(o, pst[h]);
             }
-            e = bb::launch_step(s->n, p, st);
+            if (e == hipSuccess && split && h == 0) {
+                // half B's policy pass k starts when half A's has finished:
+                // it then runs beside half A's step
+                e = hipEventRecord(s->aux_ev[1], pst[0]);
+                if (e == hipSuccess) e = hipStreamWaitEvent(pst[1], s->aux_ev[1], 0);
+            }
+            if (e == hipSuccess) {
+                bb::Params p = sp[h];
+                if (out->obs && k + 1 < n) {
+                    p.rec_obs = out->obs + (int64_t)(k + 1) * W * bb::POL_IN + pw0[h] * bb::POL_IN;
+                    p.rec_agent = trainee;
+                }
+                e = bb::launch_step(s->n, p, pst[h]);
+            }
+            if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
         }
-        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
+    }
+    if (split) {  // the caller's stream continues after part B too
+        hipError_t e = hipEventRecord(s->aux_ev[0], s->aux);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[0], 0);
+        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy join");
     }
     if (final_needed && !fused) {
         hipError_t e = bb::launch_policy(pass(n, true), st);

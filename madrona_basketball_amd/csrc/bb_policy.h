@@ -56,6 +56,8 @@ struct PolicyArgs {
     float *rew_out, *done_out;        // -> rew_out[r], done_out[r]
     uint64_t *diag_ts;                // diagnostics only: POL_TRACE_POINTS clocks of each wave's first tile
     const float *packed;              // device: the weights in k_policy_rows' order (PolicyPack), or null
+    uint32_t key_row0;                // sampling key of row r: key_row0 + r (a part of a larger call keeps its rows' keys)
+    int32_t mt;                       // k_policy<mt> forced (1, 2, 4; bb_rollout_policy's split halves), 0: by row count
 };
 
 // The weights in the order k_policy_rows consumes them (each matrix's k-chain
@@ -264,7 +266,7 @@ inline void policy_row_host(const PolicyArgs &a, int64_t r)
     }
     int32_t act[6];
     float lp;
-    pol_select(out, a.stochastic != 0, a.seed, a.step, (uint32_t)r, act, &lp);
+    pol_select(out, a.stochastic != 0, a.seed, a.step, (uint32_t)r + a.key_row0, act, &lp);
     if (a.obs_out)
         for (int k = 0; k < POL_IN; k++) a.obs_out[r * POL_IN + k] = o[k];
     if (a.actions) {

@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
             for (int i = 0; i <= POL_LOGITS; i++) logit[i] = tile[lane][i];
             int32_t act[6];
             float lp;
-            pol_select(logit, a.stochastic != 0, a.seed, a.step, (uint32_t)rr, act, &lp);
+            pol_select(logit, a.stochastic != 0, a.seed, a.step, (uint32_t)rr + a.key_row0, act, &lp);
             if (a.actions) {
                 int32_t *d = a.actions + rr * a.act_stride;
 #pragma unroll
@@ -479,7 +479,7 @@ __global__ __launch_bounds__(256) void k_policy_rows(const PolicyArgs a, const f
     }
     int32_t act[6];
     float lp;
-    pol_select(out, STOCH == 1, a.seed, a.step, (uint32_t)rr, act, &lp);
+    pol_select(out, STOCH == 1, a.seed, a.step, (uint32_t)rr + a.key_row0, act, &lp);
     if (!live) return;
     if (a.actions) {
         int32_t *d = a.actions + r * a.act_stride;
@@ -629,6 +629,12 @@ static hipError_t launch_policy_rows(const PolicyArgs &a, hipStream_t s)
 hipError_t launch_policy(const PolicyArgs &a, hipStream_t s)
 {
     if (a.rows <= 0) return hipSuccess;
+    switch (a.mt) {  // the caller's choice
+    case 1: return launch_policy_mt<1>(a, s);
+    case 2: return launch_policy_mt<2>(a, s);
+    case 4: return launch_policy_mt<4>(a, s);
+    default: break;
+    }
     if (policy_rows_enabled(a.rows)) return launch_policy_rows(a, s);
     if (policy_wg_enabled(a.rows)) {
         const int64_t tiles = (a.rows + 15) / 16;

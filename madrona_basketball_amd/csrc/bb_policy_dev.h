@@ -139,7 +139,7 @@ struct BucketNoise {
 };
 template <int R>
 __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, uint32_t step, int64_t row0, int64_t rows,
-                                             int lane)
+                                             int lane, uint32_t key0 = 0)
 {
     using BN = BucketNoise<R>;
     const int r = lane / BN::LPR, part = lane % BN::LPR;
@@ -147,7 +147,7 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
 #pragma unroll
     for (int j = 0; j < BN::BPL; j++) {
         const int b = part + BN::LPR * j;
-        n.u[j] = (b < POL_BUCKETS && rr < rows) ? pol_bucket_u(seed, step, (uint32_t)rr, b) : 0.f;
+        n.u[j] = (b < POL_BUCKETS && rr < rows) ? pol_bucket_u(seed, step, (uint32_t)rr + key0, b) : 0.f;
     }
 }
 
@@ -185,7 +185,7 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     // chain raised k_policy_wg over its register budget)
     BucketNoise<R> own;
     if constexpr (!PRE) {
-        if (stochastic) bucket_noise<R>(own, a.seed, a.step, row0, a.rows, lane);
+        if (stochastic) bucket_noise<R>(own, a.seed, a.step, row0, a.rows, lane, a.key_row0);
     }
     // bucket maxima (every lane, compile-time indices)
     float mx[POL_BUCKETS];

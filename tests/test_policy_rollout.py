@@ -135,6 +135,16 @@ def test_gpu_policy_rollout_at_65536_worlds_equals_the_ppo_loop(native_lib):
 
 
 @pytest.mark.gpu
+def test_gpu_split_policy_rollout_odd_worlds_with_opponent(native_lib):
+    """From 32 768 worlds the per-step rollout runs the two world halves on two
+    streams (bb_host.hip, shard_params): an odd count (halves of 20 001 and
+    20 000 worlds), the frozen opponent and a deterministic trainee, still ==
+    FusedPolicy.act + step per step, every output and every column."""
+    assert torch.cuda.is_available()
+    run_pair(ExecMode.CUDA, 40001, 6, 1, False, True, "cuda")
+
+
+@pytest.mark.gpu
 def test_gpu_policy_rollout_equals_host_executor(native_lib):
     """Device rollout == host-executor rollout (policy and step), bit for bit."""
     assert torch.cuda.is_available()

@@ -86,7 +86,12 @@ def trace(L, sim, stream):
     rc = L.bb_diag_trace(sim._h, stream, buf.ctypes.data, cap, ctypes.byref(nw))
     assert rc == 0, L.bb_last_error()
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 10, 50, 90, 100)]
-    ngrid = (sim.num_worlds * sim.num_agents + 63) // 64
+    # one wave per 64 // N worlds (N = 2: 32 worlds of agent lanes; N >= 4:
+    # 64 // N worlds of the LDS-world kernel, the lanes past them idle)
+    wpw = 64 // sim.num_agents
+    ngrid = (sim.num_worlds + wpw - 1) // wpw
+    if nw.value != ngrid and nw.value % ngrid:
+        raise RuntimeError(f"trace: {nw.value} wave records for a {ngrid}-wave grid")
     if nw.value != ngrid:  # k_step_wide: WAVES waves per workgroup, per-role phases
         waves = nw.value // ngrid
         t = buf[: nw.value, :10].astype(np.int64).reshape(ngrid, waves, 10)

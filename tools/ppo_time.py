@@ -6,6 +6,7 @@ python tools/ppo_time.py [--worlds 65536] [--rollouts 6]
 import argparse
 import os
 import sys
+import time
 
 import torch
 
@@ -17,6 +18,7 @@ def main():
     ap.add_argument("--worlds", type=int, default=65536)
     ap.add_argument("--rollouts", type=int, default=6)
     ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--host", action="store_true", help="also time the host's enqueue of one rollout")
     a = ap.parse_args()
     import madrona_basketball_amd as mba
     from madrona_basketball_amd.policy import FusedPolicy, make_agent
@@ -35,6 +37,14 @@ def main():
             ms = sum(pol.rollout(sim, a.k, bufs, seed=1, step0=(i + 1) * a.k, per_step=per_step, time_kernels=True)
                      for i in range(a.rollouts)) / a.rollouts
             print(f"{name:26s} per_step={int(per_step)}  {ms * 1e3 / a.k:8.2f} us/step", flush=True)
+            if a.host:  # host time to enqueue one rollout (the call returns once its launches are queued)
+                t0 = time.perf_counter()
+                pol.rollout(sim, a.k, bufs, seed=1, step0=99 * a.k, per_step=per_step)
+                t1 = time.perf_counter()
+                torch.cuda.synchronize()
+                t2 = time.perf_counter()
+                print(f"{name:26s} per_step={int(per_step)}  host enqueue {(t1 - t0) * 1e6 / a.k:8.2f} us/step, "
+                      f"enqueue + drain {(t2 - t0) * 1e6 / a.k:8.2f} us/step", flush=True)
 
 
 if __name__ == "__main__":
