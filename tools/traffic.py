@@ -7,6 +7,9 @@ streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
 streaming stores.  Infinity-Cache hits are counted (not excluded).
 
 python tools/traffic.py <fetch_dir> <write_dir> <workload_key> [--out profiles/traffic.json]
+python tools/traffic.py <fetch_dir> <write_dir> W65536_PPO_R32 --ppo 2
+    (PPO rollout: every k_policy and k_step launch summed, per step = per
+    k_step launch x the parts a step is split into -- 2 from 32 768 worlds)
 """
 import argparse
 import csv
@@ -27,25 +30,64 @@ def per_launch(d, counter, kernel_sub):
     return statistics.median(vals), len(vals)
 
 
+def ppo_per_step(d, counter, parts):
+    """Sum of counter over every k_policy / k_step launch, per PPO step."""
+    tot, steps, pol = 0.0, 0, 0.0
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] != counter:
+                continue
+            k = r["Kernel_Name"]
+            if "k_step<" in k:
+                tot += float(r["Counter_Value"])
+                steps += 1
+            elif "k_policy" in k:
+                tot += float(r["Counter_Value"])
+                pol += float(r["Counter_Value"])
+    if not steps:
+        raise SystemExit(f"no k_step {counter} rows under {d}")
+    n = steps / parts
+    return tot / n, pol / n, steps
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
     ap.add_argument("write_dir")
     ap.add_argument("key")
     ap.add_argument("--kernel", default="k_step<2, 0>")
+    ap.add_argument("--ppo", type=int, default=0, help="PPO rollout mode: parts per step (1 or 2)")
+    ap.add_argument("--note", default="")
+    ap.add_argument("--div", type=int, default=1, help="units (steps) per launch: the entry is per unit")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "traffic.json"))
     a = ap.parse_args()
-    fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
-    wk, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
-    fetch = 2.0 * fk * 1024.0
-    write = wk * 1024.0
     try:
         data = json.load(open(a.out))
     except (OSError, ValueError):
         data = {}
+    if a.ppo:
+        fk, fpol, nf = ppo_per_step(a.fetch_dir, "FETCH_SIZE", a.ppo)
+        wk, wpol, nw = ppo_per_step(a.write_dir, "WRITE_SIZE", a.ppo)
+        fetch, write = 2.0 * fk * 1024.0, wk * 1024.0
+        pol = 2.0 * fpol * 1024.0 + wpol * 1024.0
+        data[a.key] = {
+            "bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "k_policy_bytes": pol, "k_step_bytes": fetch + write - pol,
+            "per": f"PPO step ({a.ppo} part(s): every k_policy and k_step launch of the run / (k_step launches / parts))",
+            "k_step_launches": [nf, nw], "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> bytes",
+            "source": a.note,
+        }
+        json.dump(data, open(a.out, "w"), indent=1, sort_keys=True)
+        print(json.dumps(data[a.key]))
+        return
+    fk, nf = per_launch(a.fetch_dir, "FETCH_SIZE", a.kernel)
+    wk, nw = per_launch(a.write_dir, "WRITE_SIZE", a.kernel)
+    fetch = 2.0 * fk * 1024.0 / a.div
+    write = wk * 1024.0 / a.div
     data[a.key] = {
         "bytes_per_launch": fetch + write,
+        "per": "launch" if a.div == 1 else f"1/{a.div} of a launch (one step)",
         "fetch_bytes": fetch,
         "write_bytes": write,
         "raw_FETCH_SIZE_KiB": fk,
@@ -53,6 +95,7 @@ def main():
         "launches": [nf, nw],
         "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> bytes",
         "kernel": a.kernel,
+        "source": a.note,
     }
     json.dump(data, open(a.out, "w"), indent=1, sort_keys=True)
     print(json.dumps(data[a.key]))
