@@ -261,8 +261,9 @@ struct bb_sim {
     std::unique_ptr<bb::HostPool> pool;  // ExecMode.CPU workers (created with the simulator)
     // (CUDA mode) the second stream and events of bb_rollout_policy's split
     // per-step loop, created on first use
-    hipStream_t aux = nullptr;
-    hipEvent_t aux_ev[2] = {nullptr, nullptr};
+    static constexpr int MAX_PARTS = 4;
+    hipStream_t aux[MAX_PARTS - 1] = {};
+    hipEvent_t aux_ev[2 * MAX_PARTS] = {};
 };
 
 namespace {
@@ -574,12 +575,14 @@ int bb_create_with_buffers(const bb_config *cfg, void *const *bufs, int32_t nbuf
 int bb_destroy(bb_sim *s)
 {
     if (!s) return BB_OK;
-    if (s->aux) {
+    if (s->aux[0]) {
         DeviceGuard g(s->device);
-        (void)hipStreamSynchronize(s->aux);
+        for (hipStream_t a : s->aux)
+            if (a) (void)hipStreamSynchronize(a);
         for (hipEvent_t e : s->aux_ev)
             if (e) (void)hipEventDestroy(e);
-        (void)hipStreamDestroy(s->aux);
+        for (hipStream_t a : s->aux)
+            if (a) (void)hipStreamDestroy(a);
     }
     if (s->owns) {
         for (int id = 0; id < NUM_SLOTS; id++) {
@@ -934,6 +937,30 @@ static int64_t ppo_split_min_worlds()
     return v;
 }
 
+// The parts are independent worlds, so nothing orders them but the start:
+// part h's first policy pass waits for part h - 1's.  Re-aligning them every
+// step (an event per step) measured 54.5-55.7 vs 52.3-53.5 us per step
+// (profiles/r04/v_*); MADRONA_BB_PPO_SPLIT_SYNC=k re-aligns every k steps.
+static int ppo_split_sync_every()
+{
+    static const int v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_SYNC");
+        return e && *e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+// World parts of the split loop (2 .. bb_sim::MAX_PARTS), MADRONA_BB_PPO_SPLIT_PARTS
+static int ppo_split_parts()
+{
+    static const int v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_PARTS");
+        const int k = e && *e ? std::atoi(e) : 2;
+        return k < 2 ? 2 : (k > bb_sim::MAX_PARTS ? bb_sim::MAX_PARTS : k);
+    }();
+    return v;
+}
+
 // The fused PPO rollout (k_rollout_policy) runs one workgroup of 3 waves per
 // 32 worlds at one workgroup per CU (register-bound): used up to two waves of
 // workgroups -- measured 8 192 worlds 15.1 vs 27.6 us per step unfused,
@@ -1084,24 +1111,28 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         return a;
     };
     const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
-    const int parts = split ? 2 : 1;
-    const int64_t half = (W + 1) / 2;
-    hipStream_t pst[2] = {st, st};
+    const int parts = split ? ppo_split_parts() : 1;
+    constexpr int MP = bb_sim::MAX_PARTS;
+    hipStream_t pst[MP] = {st, st, st, st};
     if (split) {
-        if (!s->aux) {
-            if (hipStreamCreateWithFlags(&s->aux, hipStreamNonBlocking) != hipSuccess) return fail(BB_ERR_HIP, "hipStreamCreate");
+        if (!s->aux[0]) {
+            for (hipStream_t &a : s->aux)
+                if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) return fail(BB_ERR_HIP, "hipStreamCreate");
             for (hipEvent_t &e : s->aux_ev)
                 if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(BB_ERR_HIP, "hipEventCreate");
         }
-        pst[1] = s->aux;
-        (void)hipEventRecord(s->aux_ev[0], st);  // part B starts after everything before the call
-        (void)hipStreamWaitEvent(s->aux, s->aux_ev[0], 0);
+        // every part starts after everything before the call on the caller's stream
+        (void)hipEventRecord(s->aux_ev[0], st);
+        for (int h = 1; h < parts; h++) {
+            pst[h] = s->aux[h - 1];
+            (void)hipStreamWaitEvent(pst[h], s->aux_ev[0], 0);
+        }
     }
-    bb::Params sp[2];
-    int64_t pw0[2], pcnt[2];
+    bb::Params sp[MP];
+    int64_t pw0[MP], pcnt[MP];
     for (int h = 0; h < parts; h++) {
-        pw0[h] = split ? h * half : 0;
-        pcnt[h] = split ? (h == 0 ? half : W - half) : W;
+        pw0[h] = W * h / parts;
+        pcnt[h] = W * (h + 1) / parts - pw0[h];
         sp[h] = split ? shard_params(s->p, s->n, pw0[h], pcnt[h]) : s->p;
     }
     // buffer.obs[k + 1] (the trainee's rows after step k) is written by step
@@ -1120,11 +1151,12 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 if (split) o = part_pass(o, pw0[h], pcnt[h], sp[h]);
                 e = bb::launch_policy(o, pst[h]);
             }
-            if (e == hipSuccess && split && h == 0) {
-                // half B's policy pass k starts when half A's has finished:
-                // it then runs beside half A's step
-                e = hipEventRecord(s->aux_ev[1], pst[0]);
-                if (e == hipSuccess) e = hipStreamWaitEvent(pst[1], s->aux_ev[1], 0);
+            if (e == hipSuccess && split && h + 1 < parts &&
+                (k == 0 || (ppo_split_sync_every() > 0 && k % ppo_split_sync_every() == 0))) {
+                // part h + 1's policy pass k starts when part h's has finished:
+                // it then runs beside part h's step
+                e = hipEventRecord(s->aux_ev[1 + h], pst[h]);
+                if (e == hipSuccess) e = hipStreamWaitEvent(pst[h + 1], s->aux_ev[1 + h], 0);
             }
             if (e == hipSuccess) {
                 bb::Params p = sp[h];
@@ -1137,9 +1169,9 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
         }
     }
-    if (split) {  // the caller's stream continues after part B too
-        hipError_t e = hipEventRecord(s->aux_ev[0], s->aux);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[0], 0);
+    for (int h = 1; h < parts; h++) {  // the caller's stream continues after every part
+        hipError_t e = hipEventRecord(s->aux_ev[MP + h], pst[h]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[MP + h], 0);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy join");
     }
     if (final_needed && !fused) {
