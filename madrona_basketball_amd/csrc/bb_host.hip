@@ -919,15 +919,15 @@ bb::Params shard_params(const bb::Params &p, int N, int64_t w0, int64_t count)
 }
 
 // Split per-step PPO loop (bb_rollout_policy) from this many worlds on: the
-// two halves of the worlds run on two streams, half B's policy pass k after
-// half A's, so one half's policy pass (latency-bound) runs beside the other
-// half's step (memory-bound).  The halves' policy passes take k_policy<1>
-// (124 VGPRs: a policy wave and a step wave share a SIMD; k_policy<4>'s 240
-// do not, and then the kernels only alternate: 58.9 us per step at 65 536
-// worlds).  Measured per step, K = 32, all records (profiles/r04/r_*):
-// 32 768 worlds 41.0 -> 37.5-38.5 us, 65 536 56.1 -> 54.3-55.6, 131 072
-// 99.5 -> 92.5, 262 144 187.2 -> 176.4.  MADRONA_BB_PPO_SPLIT_MIN_WORLDS
-// overrides it (0: never split).
+// two halves of the worlds run on two streams, half B's first policy pass
+// after half A's, so one half's policy pass (latency-bound) runs beside the
+// other half's step (memory-bound).  The halves' policy passes take
+// k_policy<1> (234 VGPRs + 8 AGPRs: a policy wave and a 224-VGPR step wave
+// share a SIMD's 512; k_policy<4>'s 256 + 220 do not, and then the kernels
+// only alternate: 58.9 us per step at 65 536 worlds).  Measured per step,
+// K = 32, all records (profiles/r04/r_*, v_*): 32 768 worlds 41.0 -> 35.4 us,
+// 65 536 56.1 -> 52.3-53.9, 131 072 99.5 -> 92.5, 262 144 187.2 -> 176.4.
+// MADRONA_BB_PPO_SPLIT_MIN_WORLDS overrides it (0: never split).
 static int64_t ppo_split_min_worlds()
 {
     static const int64_t v = [] {
@@ -1107,7 +1107,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             adv(a.done_out, 1);
         }
         a.key_row0 = (uint32_t)w0;
-        a.mt = 1;  // 124 VGPRs: a policy wave fits beside a step wave on one SIMD
+        a.mt = 1;  // 242 registers: a policy wave fits beside a step wave on one SIMD
         return a;
     };
     const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
