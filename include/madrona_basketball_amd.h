@@ -244,7 +244,10 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
  * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
  * On gfx950 without an opponent (and up to 16 384 worlds) one fused launch
  * runs all n steps; flags BB_ROLLOUT_PER_STEP forces a policy launch and a
- * step launch per step instead.
+ * step launch per step instead.  From 32 768 worlds the per-step launches of
+ * two world halves go to `stream` and to a second stream the simulator owns
+ * (created on first use, destroyed by bb_destroy); `stream` waits for both
+ * before the call's last work, so stream order holds for the caller.
  * kernel_ms (CUDA mode): time from the first launch to the last, after a sync. */
 typedef struct bb_policy_rollout_buffers {
     float *obs;
