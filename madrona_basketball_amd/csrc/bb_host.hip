@@ -922,11 +922,12 @@ bb::Params shard_params(const bb::Params &p, int N, int64_t w0, int64_t count)
 // two halves of the worlds run on two streams, half B's first policy pass
 // after half A's, so one half's policy pass (latency-bound) runs beside the
 // other half's step (memory-bound).  The halves' policy passes take
-// k_policy<1> (234 VGPRs + 8 AGPRs: a policy wave and a 224-VGPR step wave
+// k_policy<2> (256 VGPRs + 19 AGPRs: a policy wave and a 224-VGPR step wave
 // share a SIMD's 512; k_policy<4>'s 256 + 220 do not, and then the kernels
 // only alternate: 58.9 us per step at 65 536 worlds).  Measured per step,
-// K = 32, all records (profiles/r04/r_*, v_*): 32 768 worlds 41.0 -> 35.4 us,
-// 65 536 56.1 -> 52.3-53.9, 131 072 99.5 -> 92.5, 262 144 187.2 -> 176.4.
+// K = 32, all records (profiles/r04/r_*, v_*, z_*): 32 768 worlds 41.0 ->
+// 35.4 us, 65 536 56.1 -> 50.1-51.3 (k_policy<1> halves 51.9-53.2,
+// k_policy_wg 54.7-55.5), 131 072 99.5 -> 92.5, 262 144 187.2 -> 176.4.
 // MADRONA_BB_PPO_SPLIT_MIN_WORLDS overrides it (0: never split).
 static int64_t ppo_split_min_worlds()
 {
@@ -946,6 +947,17 @@ static int ppo_split_sync_every()
     static const int v = [] {
         const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_SYNC");
         return e && *e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
+// The parts' policy kernel: k_policy<MT> (1, 2, 4; default 2), 0: launch_policy's
+// own choice for the part's rows (MADRONA_BB_POLICY_WG=1 then forces k_policy_wg)
+static int ppo_split_mt()
+{
+    static const int v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_MT");
+        return e && *e ? std::atoi(e) : 2;
     }();
     return v;
 }
@@ -1107,7 +1119,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             adv(a.done_out, 1);
         }
         a.key_row0 = (uint32_t)w0;
-        a.mt = 1;  // 242 registers: a policy wave fits beside a step wave on one SIMD
+        a.mt = ppo_split_mt();  // k_policy<2>: 276 registers, a policy wave fits beside a step wave on one SIMD
         return a;
     };
     const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();

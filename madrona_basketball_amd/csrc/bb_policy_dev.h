@@ -41,6 +41,11 @@ __device__ __forceinline__ float dpp_f(float x)
 {
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
 }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t x)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
 __device__ __forceinline__ float quarter_sum(float t)
 {
     t = t + dpp_f<0xB1>(t);   // quad_perm [1,0,3,2]: xor 1
@@ -144,6 +149,22 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
     using BN = BucketNoise<R>;
     const int r = lane / BN::LPR, part = lane % BN::LPR;
     const int64_t rr = row0 + r;
+    if constexpr (R == 16) {
+        // 4 lanes per row (a DPP quad), buckets part and part + 4: three
+        // threefry calls per row, one per lane -- part 0 the pair of buckets
+        // 0 / 1, part 1 buckets 4 / 5, parts 2 and 3 buckets 2 / 3 -- and the
+        // words handed over by quad_perm moves (one call per lane instead of
+        // two; the same words pol_bucket_u draws)
+        uint32_t pm = part == 0 ? 0u : (part == 1 ? 2u : 1u);
+        uint32_t w0, w1;
+        threefry2x32(seed, step, (uint32_t)rr + key0, pm, &w0, &w1);
+        const bool odd = (part & 1) != 0, live = rr < rows;
+        const uint32_t a0 = dpp_u<0xA0>(w0), a1 = dpp_u<0xA0>(w1);  // quad_perm [0,0,2,2]: buckets 0-3
+        const uint32_t c0 = dpp_u<0x55>(w0), c1 = dpp_u<0x55>(w1);  // quad_perm [1,1,1,1]: buckets 4, 5
+        n.u[0] = live ? pol_u01(odd ? a1 : a0) : 0.f;
+        n.u[1] = (live && part < 2) ? pol_u01(odd ? c1 : c0) : 0.f;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < BN::BPL; j++) {
         const int b = part + BN::LPR * j;
