@@ -12,4 +12,4 @@ for cfg in "1 0" "1 1024" "1 2048" "1 3072" "2 0" "2 1024" "2 2048" "4 0" "4 512
     echo "MT=$1 GRID=$2"
     MADRONA_BB_POLICY_MT=$1 timeout -k 10 120 python3 tools/policy_time.py --worlds 65536 2>&1 | grep -v amdgpu.ids | grep "agent 0" || exit 1
 done
-bash tools/gpu_r04e.sh
+bash tools/sessions/gpu_r04e.sh
