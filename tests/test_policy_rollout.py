@@ -145,6 +145,31 @@ def test_gpu_split_policy_rollout_odd_worlds_with_opponent(native_lib):
 
 
 @pytest.mark.gpu
+def test_gpu_split_policy_rollout_on_a_side_stream(native_lib):
+    """The split rollout (from 32 768 worlds: a second stream inside the call)
+    issued on a torch side stream: clones enqueued on that stream right after
+    the call see every part's records and final state, equal to the PPO loop."""
+    assert torch.cuda.is_available()
+    W, n = 32768, 4
+    sims = [make_sim(ExecMode.CUDA, W, per_world_rng=True) for _ in range(2)]
+    for s in sims:
+        s.step_n(5, random_actions=True, action_seed=321, step0=0)
+    torch.cuda.synchronize()
+    pol = FusedPolicy.from_agent(make_agent(6).cuda())
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        bufs = pol.rollout_buffers(sims[0], n)
+        pol.rollout(sims[0], n, bufs, stochastic=True, seed=9, step0=2)
+        snap = {k: v.clone() for k, v in bufs.items()}
+        views = {k: v.clone() for k, v in sims[0]._views.items()}
+    ref = reference_loop(sims[1], pol, n, stochastic=True, seed=9, step0=2)
+    torch.cuda.synchronize()
+    assert_same(snap, ref)
+    for name in views:
+        assert torch.equal(views[name], sims[1]._views[name]), name
+
+
+@pytest.mark.gpu
 def test_gpu_policy_rollout_equals_host_executor(native_lib):
     """Device rollout == host-executor rollout (policy and step), bit for bit."""
     assert torch.cuda.is_available()
