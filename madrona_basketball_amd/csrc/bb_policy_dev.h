@@ -165,6 +165,21 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
         n.u[1] = (live && part < 2) ? pol_u01(odd ? c1 : c0) : 0.f;
         return;
     }
+    if constexpr (R == 32) {
+        // 2 lanes per row, buckets part, part + 2, part + 4 (words `part` of
+        // pairs 0, 1, 2): pair `part` and pair 2 per lane, pair 1 - part's
+        // words from the row's other lane (quad_perm [1,0,3,2]): two threefry
+        // calls per lane instead of three
+        uint32_t a0, a1, b0, b1;
+        threefry2x32(seed, step, (uint32_t)rr + key0, (uint32_t)part, &a0, &a1);
+        threefry2x32(seed, step, (uint32_t)rr + key0, 2u, &b0, &b1);
+        const uint32_t x0 = dpp_u<0xB1>(a0), x1 = dpp_u<0xB1>(a1);
+        const bool live = rr < rows;
+        n.u[0] = live ? pol_u01(part ? x1 : a0) : 0.f;
+        n.u[1] = live ? pol_u01(part ? a1 : x0) : 0.f;
+        n.u[2] = live ? pol_u01(part ? b1 : b0) : 0.f;
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < BN::BPL; j++) {
         const int b = part + BN::LPR * j;
