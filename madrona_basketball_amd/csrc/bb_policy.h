@@ -154,9 +154,9 @@ BB_HD constexpr int pol_bucket_off(int b) { return b == 0 ? 0 : (b == 1 ? 2 : (b
 
 // Bucket B of one row: its action (argmax or inverse-CDF sample) and the
 // log-prob term logit[a] - logsumexp(bucket).
+// u: the bucket's uniform (pol_bucket_u), read only when stochastic.
 template <int B>
-BB_HD void pol_bucket_term(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
-                           int32_t *act, float *term)
+BB_HD void pol_bucket_term(const float *logit, bool stochastic, float u, int32_t *act, float *term)
 {
     constexpr int o = pol_bucket_off(B), nb = pol_bucket(B);
     float mx = logit[o];
@@ -170,7 +170,7 @@ BB_HD void pol_bucket_term(const float *logit, bool stochastic, uint32_t seed, u
     }
     int a = 0;
     if (stochastic) {
-        a = pol_inverse_cdf(e, nb, s, pol_bucket_u(seed, step, row, B));
+        a = pol_inverse_cdf(e, nb, s, u);
     } else {
         float best = logit[o];
 #pragma unroll
@@ -199,13 +199,24 @@ BB_HD float pol_logp_sum(const float (&term)[POL_BUCKETS])
 BB_HD void pol_select(const float *logit, bool stochastic, uint32_t seed, uint32_t step, uint32_t row,
                       int32_t act[6], float *logp_sum)
 {
+    // the six uniforms (pol_bucket_u's values): one threefry call per bucket pair
+    float u[POL_BUCKETS] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (stochastic) {
+#pragma unroll
+        for (int p = 0; p < POL_BUCKETS / 2; p++) {
+            uint32_t b0, b1;
+            threefry2x32(seed, step, row, (uint32_t)p, &b0, &b1);
+            u[2 * p] = pol_u01(b0);
+            u[2 * p + 1] = pol_u01(b1);
+        }
+    }
     float term[POL_BUCKETS];
-    pol_bucket_term<0>(logit, stochastic, seed, step, row, &act[0], &term[0]);
-    pol_bucket_term<1>(logit, stochastic, seed, step, row, &act[1], &term[1]);
-    pol_bucket_term<2>(logit, stochastic, seed, step, row, &act[2], &term[2]);
-    pol_bucket_term<3>(logit, stochastic, seed, step, row, &act[3], &term[3]);
-    pol_bucket_term<4>(logit, stochastic, seed, step, row, &act[4], &term[4]);
-    pol_bucket_term<5>(logit, stochastic, seed, step, row, &act[5], &term[5]);
+    pol_bucket_term<0>(logit, stochastic, u[0], &act[0], &term[0]);
+    pol_bucket_term<1>(logit, stochastic, u[1], &act[1], &term[1]);
+    pol_bucket_term<2>(logit, stochastic, u[2], &act[2], &term[2]);
+    pol_bucket_term<3>(logit, stochastic, u[3], &act[3], &term[3]);
+    pol_bucket_term<4>(logit, stochastic, u[4], &act[4], &term[4]);
+    pol_bucket_term<5>(logit, stochastic, u[5], &act[5], &term[5]);
     *logp_sum = pol_logp_sum(term);
 }
 
