@@ -962,6 +962,17 @@ static int ppo_split_mt()
     return v;
 }
 
+// (A/B) MADRONA_BB_PPO_REC_ONLY=0: the per-step loop's steps also write the
+// trainee's rows into the sim's obs (and the policy reads them there)
+static bool ppo_rec_only()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_REC_ONLY");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 // World parts of the split loop (2 .. bb_sim::MAX_PARTS), MADRONA_BB_PPO_SPLIT_PARTS
 static int ppo_split_parts()
 {
@@ -1105,7 +1116,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         const auto adv = [&](auto *&ptr, int64_t per) {
             if (ptr) ptr += w0 * per;
         };
-        a.obs += w0 * N * ow;
+        a.obs += w0 * a.obs_stride;
         a.rows = cnt;
         adv(a.actions, N * 6);
         adv(a.obs_out, bb::POL_IN);
@@ -1123,6 +1134,10 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         return a;
     };
     const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
+    // steps 0 .. n-2 write the trainee's rows into buffer.obs[k + 1] only (the
+    // sim's copy of them is read by nobody before the last step rewrites
+    // every row); the next policy pass reads them there
+    const bool rec_only = out->obs != nullptr && ppo_rec_only();
     const int parts = split ? ppo_split_parts() : 1;
     constexpr int MP = bb_sim::MAX_PARTS;
     hipStream_t pst[MP] = {st, st, st, st};
@@ -1156,6 +1171,10 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         for (int h = 0; h < parts; h++) {
             bb::PolicyArgs a = pass(k, false);
             if (k > 0) a.obs_out = nullptr;
+            if (k > 0 && rec_only) {  // the rows step k - 1 wrote into buffer.obs[k] only
+                a.obs = out->obs + (int64_t)k * W * bb::POL_IN;
+                a.obs_stride = bb::POL_IN;
+            }
             if (split) a = part_pass(a, pw0[h], pcnt[h], sp[h]);
             hipError_t e = bb::launch_policy(a, pst[h]);
             if (e == hipSuccess && opponent) {
@@ -1175,6 +1194,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 if (out->obs && k + 1 < n) {
                     p.rec_obs = out->obs + (int64_t)(k + 1) * W * bb::POL_IN + pw0[h] * bb::POL_IN;
                     p.rec_agent = trainee;
+                    p.rec_only = rec_only ? 1 : 0;
                 }
                 e = bb::launch_step(s->n, p, pst[h]);
             }

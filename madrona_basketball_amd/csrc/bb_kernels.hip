@@ -360,6 +360,7 @@ __device__ __forceinline__ void row_store(char *base, uint32_t off, vf4 v)
 struct RecRows {
     char *base;
     int agent;
+    bool only;  // the agent's rows into the record only (Params::rec_only)
 };
 #ifndef BB_REC_AUX
 #define BB_REC_AUX 2  // record rows: non-temporal (a fresh [K][W][128] buffer, beyond the cache for K >= 8)
@@ -377,13 +378,14 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
     for (int b0 = 0; b0 < QT; b0 += BS) {
         vf4 v[BS];
         uint32_t go[BS], ro[BS];
-        bool ok[BS], rk[BS];
+        bool ok[BS], rk[BS], sk[BS];
 #pragma unroll
         for (int j = 0; j < BS; j++) {
             if (b0 + j < QT) {
                 ok[j] = (QN == QT || q < QN) && (ALL || ((staged >> r) & 1ull));
                 go[j] = (uint32_t)(r * (RSTR * OW * 4) + q * 16);
                 rk[j] = ok[j] && (r % N) == rec.agent;
+                sk[j] = ok[j] && !(rec.only && (r % N) == rec.agent);
                 ro[j] = (uint32_t)((r / N) * (OW * 4) + q * 16);
                 if (ok[j]) {
                     v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
@@ -396,7 +398,7 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
         }
 #pragma unroll
         for (int j = 0; j < BS; j++)
-            if (b0 + j < QT && ok[j]) row_store<AUX>(base, go[j], v[j]);
+            if (b0 + j < QT && sk[j]) row_store<AUX>(base, go[j], v[j]);
         if (rec.base) {  // wave-uniform
 #pragma unroll
             for (int j = 0; j < BS; j++)
@@ -407,7 +409,7 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
 
 template <int N, int QT, int RS, int Q0, int QN, int RSTR, int QZ = QN, int AUX = -1>
 __device__ __forceinline__ void flush_tile(const float *tile, float *obs, int64_t row0, uint64_t staged, int lane,
-                                           RecRows rec = RecRows{nullptr, 0})
+                                           RecRows rec = RecRows{nullptr, 0, false})
 {
     char *base = (char *)(obs + row0 * obs_width(N) + 4 * Q0);  // wave-uniform
     if (rec.base) rec.base += 16 * Q0;
@@ -434,7 +436,7 @@ __device__ __forceinline__ void emit_phase(const World<N> &v, const Ctx &c, cons
 template <int N, int MODE, class T, int PHASE = 0>
 __device__ __forceinline__ void obs_phases(const World<N> &v, const Ctx &c, const SharedObs<N> &sh, bool share,
                                            bool fast, float *tile, float *obs, int64_t row0, int lane, int32_t ib,
-                                           RecRows rec = RecRows{nullptr, 0})
+                                           RecRows rec = RecRows{nullptr, 0, false})
 {
     if (fast) emit_phase<N, T, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     __syncthreads();
@@ -538,10 +540,11 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
         }
     } else {
         // PPO's buffer.obs record of agent rec_agent (Params::rec_obs, N = 2)
-        RecRows rec{nullptr, 0};
-        if constexpr (REC) rec = RecRows{(char *)(c.p->rec_obs + w0 * (int64_t)OW), c.p->rec_agent};
+        RecRows rec{nullptr, 0, false};
+        if constexpr (REC)
+            rec = RecRows{(char *)(c.p->rec_obs + w0 * (int64_t)OW), c.p->rec_agent, c.p->rec_only != 0};
         if (active && !fast) {
-            fill_obs_slow(v, c, 0, grow, ib);
+            if (!(rec.base && rec.only && k == rec.agent)) fill_obs_slow(v, c, 0, grow, ib);
             if (rec.base && k == rec.agent) fill_obs_slow(v, c, 0, c.p->rec_obs + w * (int64_t)OW, ib);
         }
         obs_phases<N, MODE, T>(v, c, sh, share, fast, tile, obs, w0 * N, lane, ib, rec);

@@ -342,6 +342,10 @@ struct Params {
     // world w to rec_obs + w * 128 (the whole 128 floats, zero tail included)
     float *rec_obs;
     int32_t rec_agent;
+    // with rec_obs: agent rec_agent's row goes to rec_obs only, not to the
+    // sim's obs (PPO's per-step loop reads it there; the last step of the
+    // rollout writes every row as usual)
+    int32_t rec_only;
 };
 
 BB_HD uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
