@@ -1201,12 +1201,18 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
         }
     }
+    if (final_needed && split) {  // each part's value pass on its own stream, beside the others' last steps
+        for (int h = 0; h < parts; h++) {
+            hipError_t e = bb::launch_policy(part_pass(pass(n, true), pw0[h], pcnt[h], sp[h]), pst[h]);
+            if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
+        }
+    }
     for (int h = 1; h < parts; h++) {  // the caller's stream continues after every part
         hipError_t e = hipEventRecord(s->aux_ev[MP + h], pst[h]);
         if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[MP + h], 0);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy join");
     }
-    if (final_needed && !fused) {
+    if (final_needed && !fused && !split) {
         hipError_t e = bb::launch_policy(pass(n, true), st);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
     }
