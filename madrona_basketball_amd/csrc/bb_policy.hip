@@ -524,13 +524,18 @@ inline PolicyWgGrid policy_wg_grid(int64_t tiles)
 }
 
 // M-tiles per wave.  4: 64 rows per wave, one row per lane in the bucket
-// pass, each lane's buckets in series; 1: 16 rows per wave, 4 lanes
-// per row in the bucket pass.  Measured (profiles/r03/e_policy_mt_ab.txt):
-// 8 192 rows 18.1 (MT 4) -> 13.9-18.6 us (MT 1), 65 536 rows 24.8 (MT 4) vs
-// 28.8 us (MT 1): MT = 1 below POLICY_MT4_ROWS rows.  MADRONA_BB_POLICY_MT
-// forces one (A/B timing).
+// pass, each lane's buckets in series; 2: 32 rows, 2 lanes per row; 1: 16
+// rows per wave, 4 lanes per row in the bucket pass.  Measured
+// (profiles/r03/e_policy_mt_ab.txt, profiles/r04/mt_sweep_rows.txt; sampled,
+// us per launch): 16 384 rows MT 1 10.9 / MT 2 12.6 / MT 4 17.5; 24 576
+// 14.2 / 13.9 / 19.6; 32 768 16.4 / 15.3 / 19.9; 49 152 24.3 / 27.6 / 22.0;
+// 65 536 27.0 / 27.7 / 23.5 -- MT 2 while its waves (276 registers, one per
+// SIMD) fit one round, MT 4 above.  MADRONA_BB_POLICY_MT forces one (A/B).
+#ifndef POLICY_MT2_ROWS
+#define POLICY_MT2_ROWS 20480
+#endif
 #ifndef POLICY_MT4_ROWS
-#define POLICY_MT4_ROWS 32768
+#define POLICY_MT4_ROWS 32769
 #endif
 inline int policy_mt(int64_t rows)
 {
@@ -540,7 +545,7 @@ inline int policy_mt(int64_t rows)
         return (m == 1 || m == 2 || m == 4) ? m : 0;
     }();
     if (forced) return forced;
-    return rows < POLICY_MT4_ROWS ? 1 : 4;
+    return rows < POLICY_MT2_ROWS ? 1 : (rows < POLICY_MT4_ROWS ? 2 : 4);
 }
 
 template <int MT>
