@@ -93,11 +93,6 @@ int step_grid_n(int n, int64_t num_worlds);
 hipError_t launch_random_actions(int n, const Params &p, uint32_t seed, uint32_t step, hipStream_t s);
 hipError_t launch_poke(int32_t *dst, int count, const int32_t *vals, hipStream_t s);
 hipError_t launch_policy(const PolicyArgs &a, hipStream_t s);
-// the weights in k_policy_rows' order (PolicyPack::FLOATS floats at pk)
-hipError_t launch_policy_pack(const PolicyWeights &w, float *pk, hipStream_t s);
-// whether launch_policy would take k_policy_rows at this row count (which
-// then reads PolicyArgs::packed, or packs for the call itself)
-bool policy_wants_pack(int64_t rows);
 void host_policy(const PolicyArgs &a);
 hipError_t launch_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst, hipStream_t s);
 void host_record(const RecordArgs &a, int64_t world0, int32_t count, uint32_t *dst);

@@ -55,22 +55,10 @@ struct PolicyArgs {
     int64_t rd_stride;
     float *rew_out, *done_out;        // -> rew_out[r], done_out[r]
     uint64_t *diag_ts;                // diagnostics only: POL_TRACE_POINTS clocks of each wave's first tile
-    const float *packed;              // device: the weights in k_policy_rows' order (PolicyPack), or null
     uint32_t key_row0;                // sampling key of row r: key_row0 + r (a part of a larger call keeps its rows' keys)
     int32_t mt;                       // k_policy<mt> forced (1, 2, 4; bb_rollout_policy's split halves), 0: by row count
 };
 
-// The weights in the order k_policy_rows consumes them (each matrix's k-chain
-// order as the host and the MFMA kernels run it), written once per call or
-// rollout by k_policy_pack:
-//   P1[j][q][n] = W1[n][32q + j]     P2[j][q][n] = W2[n][8q + j]
-//   PH[j][q][m] = head_w[m][8q + j]  (m < 20: 19 logits + the value)
-// then obs_mean, obs_inv, b1, ln1_w, ln1_b, b2, ln2_w, ln2_b, head_b[0..19].
-struct PolicyPack {
-    static constexpr int HEADS = POL_LOGITS + 1;
-    static constexpr int P1 = 0, P2 = P1 + 32 * 4 * 32, PH = P2 + 8 * 4 * 32, MEAN = PH + 8 * 4 * HEADS,
-                         INV = MEAN + POL_IN, CST = INV + POL_IN, HB = CST + 6 * POL_HID, FLOATS = (HB + HEADS + 15) & ~15;
-};
 constexpr int POL_TRACE_POINTS = 8;
 
 // exp / log in f32 from a fixed sequence of f32 operations (identical bits on

@@ -335,177 +335,6 @@ __global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a
     }
 }
 
-// ---------------------------------------------------------------------------
-// k_policy_rows: one observation row per lane, 64 rows per wave, plain VALU.
-// The f32 MFMA runs at the packed-FMA rate (MI355X_MICROARCH.md: 64 FLOP/clk
-// per SIMD either way), so a lane that owns a whole row does the network's
-// 6 144 multiply-adds as v_pk_fma_f32 pairs with the weights as wave-uniform
-// scalar operands (scalar loads of PolicyPack, in consumption order), its two
-// LayerNorms and the bucket pass in its own registers: no operand transposes,
-// no LDS, no cross-lane sums.  Every value is the host's (policy_row_host:
-// the same k-ordered fmaf chains, pol_layernorm_relu, pol_select), hence the
-// MFMA kernels' too.
-typedef float pf2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ pf2 pk_fma(float x, pf2 w, pf2 acc)
-{
-    return __builtin_elementwise_fma(pf2{x, x}, w, acc);
-}
-
-__global__ __launch_bounds__(256) void k_policy_pack(const PolicyWeights w, float *pk)
-{
-    using P = PolicyPack;
-    const int i = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (i >= P::FLOATS) return;
-    float v = 0.f;
-    if (i < P::P2) {
-        const int j = i >> 7, q = (i >> 5) & 3, n = i & 31;
-        v = w.w1[n * POL_IN + 32 * q + j];
-    } else if (i < P::PH) {
-        const int t = i - P::P2, j = t >> 7, q = (t >> 5) & 3, n = t & 31;
-        v = w.w2[n * POL_HID + 8 * q + j];
-    } else if (i < P::MEAN) {
-        const int t = i - P::PH, jq = t / P::HEADS, m = t % P::HEADS, j = jq >> 2, q = jq & 3;
-        v = w.head_w[m * POL_HID + 8 * q + j];
-    } else if (i < P::INV) {
-        v = w.obs_mean[i - P::MEAN];
-    } else if (i < P::CST) {
-        v = w.obs_inv[i - P::INV];
-    } else if (i < P::HB) {
-        const int t = i - P::CST;
-        const float *src[6] = {w.b1, w.ln1_w, w.ln1_b, w.b2, w.ln2_w, w.ln2_b};
-        v = src[t >> 5][t & 31];
-    } else if (i < P::HB + P::HEADS) {
-        v = w.head_b[i - P::HB];
-    }
-    pk[i] = v;
-}
-
-// The 16 weight pairs of one k (scalar registers).  The pointer goes
-// through an empty asm per k, so the compiler cannot hoist later k's scalar
-// loads (it did: hundreds of live SGPRs, spilled to VGPR lanes); the next
-// k's loads are issued by hand one k ahead of their FMAs.
-template <int NP>
-struct WRow {
-    pf2 w[NP];
-};
-template <int NP>
-__device__ __forceinline__ WRow<NP> wrow(const float *p)
-{
-    WRow<NP> r;
-#pragma unroll
-    for (int m = 0; m < NP; m++) r.w[m] = ((const pf2 *)p)[m];
-    return r;
-}
-__device__ __forceinline__ int opaque(int off)
-{
-    __asm__ volatile("" : "+s"(off));
-    return off;
-}
-// One dense layer over a chain of K steps (k = chain order): acc[m] +=
-// x(step) * W[step][2m..2m+1]; the weights of step t at wp + t * STRIDE.
-template <int K, int NP, int STRIDE, class X>
-__device__ __forceinline__ void dense_chain(const float *wp, X x, pf2 (&acc)[NP])
-{
-    WRow<NP> cur = wrow<NP>(wp + opaque(0));
-#pragma unroll
-    for (int t = 0; t < K; t++) {
-        WRow<NP> nxt;
-        if (t + 1 < K) nxt = wrow<NP>(wp + opaque((t + 1) * STRIDE));
-        const float xt = x(t);
-#pragma unroll
-        for (int m = 0; m < NP; m++) acc[m] = pk_fma(xt, cur.w[m], acc[m]);
-        if (t + 1 < K) cur = nxt;
-    }
-}
-
-template <int STOCH>
-__global__ __launch_bounds__(256) void k_policy_rows(const PolicyArgs a, const float *__restrict__ pk)
-{
-    using P = PolicyPack;
-    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const bool live = r < a.rows;
-    const int64_t rr = live ? r : a.rows - 1;  // tail lanes compute the last row and store nothing
-    const float *o = a.obs + rr * a.obs_stride;
-    // the row (128 floats) and its record into buffer.obs (ppo.py:129)
-    float4 raw[32];
-#pragma unroll
-    for (int v = 0; v < 32; v++) raw[v] = *(const float4 *)(o + 4 * v);
-    if (a.obs_out && live) {
-        float *rec = a.obs_out + r * POL_IN;
-#pragma unroll
-        for (int v = 0; v < 32; v++) *(float4 *)(rec + 4 * v) = raw[v];
-    }
-    // RunningMeanStd clamp (agent.py:28-38), then layer 1 in the host's chain
-    // order: step t = 4j + q is k = 32q + j
-    float x[POL_IN];
-#pragma unroll
-    for (int k = 0; k < POL_IN; k++) {
-        const float4 v4 = raw[k >> 2];
-        const float v = (k & 3) == 0 ? v4.x : (k & 3) == 1 ? v4.y : (k & 3) == 2 ? v4.z : v4.w;
-        x[k] = pol_clamp((v - pk[P::MEAN + k]) * pk[P::INV + k]);
-    }
-    pf2 acc[16];
-#pragma unroll
-    for (int m = 0; m < 16; m++) acc[m] = pf2{0.f, 0.f};
-    dense_chain<128, 16, 32>(pk + P::P1, [&](int t) { return x[32 * (t & 3) + (t >> 2)]; }, acc);
-    float h[POL_HID];
-#pragma unroll
-    for (int m = 0; m < 16; m++) {
-        h[2 * m] = acc[m].x + pk[P::CST + 2 * m];
-        h[2 * m + 1] = acc[m].y + pk[P::CST + 2 * m + 1];
-    }
-    pol_layernorm_relu(h, pk + P::CST + 32, pk + P::CST + 64);
-    // layer 2 (step t = 4j + q is k = 8q + j)
-#pragma unroll
-    for (int m = 0; m < 16; m++) acc[m] = pf2{0.f, 0.f};
-    dense_chain<32, 16, 32>(pk + P::P2, [&](int t) { return h[8 * (t & 3) + (t >> 2)]; }, acc);
-#pragma unroll
-    for (int m = 0; m < 16; m++) {
-        h[2 * m] = acc[m].x + pk[P::CST + 96 + 2 * m];
-        h[2 * m + 1] = acc[m].y + pk[P::CST + 96 + 2 * m + 1];
-    }
-    pol_layernorm_relu(h, pk + P::CST + 128, pk + P::CST + 160);
-    // heads: 19 logits + the value
-    pf2 hacc[P::HEADS / 2];
-#pragma unroll
-    for (int m = 0; m < P::HEADS / 2; m++) hacc[m] = pf2{0.f, 0.f};
-    dense_chain<32, P::HEADS / 2, P::HEADS>(pk + P::PH, [&](int t) { return h[8 * (t & 3) + (t >> 2)]; }, hacc);
-    float out[P::HEADS];
-#pragma unroll
-    for (int m = 0; m < P::HEADS / 2; m++) {
-        out[2 * m] = hacc[m].x + pk[P::HB + 2 * m];
-        out[2 * m + 1] = hacc[m].y + pk[P::HB + 2 * m + 1];
-    }
-    int32_t act[6];
-    float lp;
-    pol_select(out, STOCH == 1, a.seed, a.step, (uint32_t)rr + a.key_row0, act, &lp);
-    if (!live) return;
-    if (a.actions) {
-        int32_t *d = a.actions + r * a.act_stride;
-#pragma unroll
-        for (int b = 0; b < 6; b++) d[b] = act[b];
-    }
-    if (a.act_out) {
-        int2 *d = (int2 *)(a.act_out + r * 6);
-        d[0] = make_int2(act[0], act[1]);
-        d[1] = make_int2(act[2], act[3]);
-        d[2] = make_int2(act[4], act[5]);
-    }
-    if (a.log_prob) a.log_prob[r] = lp;
-    if (a.value) a.value[r] = out[POL_LOGITS];
-    if (a.rew_out) {  // the previous step's outcome of this row (buffer.rewards / not_dones)
-        a.rew_out[r] = a.rew_src[r * a.rd_stride];
-        a.done_out[r] = a.done_src[r * a.rd_stride];
-    }
-}
-
-hipError_t launch_policy_pack(const PolicyWeights &w, float *pk, hipStream_t s)
-{
-    hipLaunchKernelGGL(k_policy_pack, dim3((PolicyPack::FLOATS + 255) / 256), dim3(256), 0, s, w, pk);
-    return hipGetLastError();
-}
-
 // Waves per workgroup and workgroups of a k_policy_wg launch: one workgroup
 // per CU (256) once there are 12 tiles per CU, fewer waves per workgroup
 // below that so that every CU gets work.
@@ -587,50 +416,6 @@ static bool policy_wg_enabled(int64_t rows)
     return forced >= 0 ? forced == 1 : rows >= POLICY_WG_MIN_ROWS;
 }
 
-// k_policy_rows: bit-identical (tests/test_policy_wg.py forces it), but as
-// compiled it keeps too many weights live in scalar registers (spilled to
-// VGPR lanes) and waits on each scalar load: 81 / 153 us at 65 536 rows
-// against k_policy<4>'s 25 / 30 (profiles/r04/c_*).  Off by default
-// (POLICY_ROWS_MIN); MADRONA_BB_POLICY_ROWS=1 / 0 forces it on / off.
-#ifndef POLICY_ROWS_MIN
-#define POLICY_ROWS_MIN (int64_t(1) << 62)
-#endif
-static bool policy_rows_enabled(int64_t rows)
-{
-    static const int forced = [] {
-        const char *e = getenv("MADRONA_BB_POLICY_ROWS");
-        return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
-    }();
-    return forced >= 0 ? forced == 1 : rows >= POLICY_ROWS_MIN;
-}
-
-bool policy_wants_pack(int64_t rows) { return policy_rows_enabled(rows); }
-
-static hipError_t launch_policy_rows(const PolicyArgs &a, hipStream_t s)
-{
-    const float *pk = a.packed;
-    float *own = nullptr;
-    if (!pk) {  // packed here, for this call only (stream-ordered scratch)
-        hipError_t e = hipMallocAsync((void **)&own, PolicyPack::FLOATS * sizeof(float), s);
-        if (e != hipSuccess) return e;
-        e = launch_policy_pack(a.w, own, s);
-        if (e != hipSuccess) {
-            (void)hipFreeAsync(own, s);
-            return e;
-        }
-        pk = own;
-    }
-    const dim3 grid((unsigned)((a.rows + 255) / 256)), block(256);
-    if (a.stochastic) hipLaunchKernelGGL(k_policy_rows<1>, grid, block, 0, s, a, pk);
-    else hipLaunchKernelGGL(k_policy_rows<0>, grid, block, 0, s, a, pk);
-    hipError_t e = hipGetLastError();
-    if (own) {
-        const hipError_t f = hipFreeAsync(own, s);
-        if (e == hipSuccess) e = f;
-    }
-    return e;
-}
-
 hipError_t launch_policy(const PolicyArgs &a, hipStream_t s)
 {
     if (a.rows <= 0) return hipSuccess;
@@ -640,7 +425,6 @@ hipError_t launch_policy(const PolicyArgs &a, hipStream_t s)
     case 4: return launch_policy_mt<4>(a, s);
     default: break;
     }
-    if (policy_rows_enabled(a.rows)) return launch_policy_rows(a, s);
     if (policy_wg_enabled(a.rows)) {
         const int64_t tiles = (a.rows + 15) / 16;
         if (tiles <= 0) return hipSuccess;

@@ -64,11 +64,23 @@ static void init_court(void)
 
 /* ---------------------------------------------------------------- math mode */
 static int g_math = OR_MATH_CR;
-static float m_sinf(float x) { return g_math == OR_MATH_LIBM ? sinf(x) : (float)sin((double)x); }
-static float m_cosf(float x) { return g_math == OR_MATH_LIBM ? cosf(x) : (float)cos((double)x); }
-static float m_atan2f(float y, float x) { return g_math == OR_MATH_LIBM ? atan2f(y, x) : (float)atan2((double)y, (double)x); }
-static float m_atanf(float x) { return g_math == OR_MATH_LIBM ? atanf(x) : (float)atan((double)x); }
-static float m_acosf(float x) { return g_math == OR_MATH_LIBM ? acosf(x) : (float)acos((double)x); }
+static float m_sinf(float x) { return g_math != OR_MATH_CR ? sinf(x) : (float)sin((double)x); }
+static float m_cosf(float x) { return g_math != OR_MATH_CR ? cosf(x) : (float)cos((double)x); }
+static float m_atan2f(float y, float x) { return g_math != OR_MATH_CR ? atan2f(y, x) : (float)atan2((double)y, (double)x); }
+static float m_atanf(float x) { return g_math != OR_MATH_CR ? atanf(x) : (float)atan((double)x); }
+static float m_acosf(float x) { return g_math != OR_MATH_CR ? acosf(x) : (float)acos((double)x); }
+/* The unqualified erf / acos / exp of game.cpp:746,808,868 on float arguments:
+ * the double overloads (C's ::erf etc., promoted argument) unless the build's
+ * headers put the float overloads into the global namespace.
+ * OR_MATH_LIBM_FLOAT binds them to erff / acosf / expf, to measure how far a
+ * reference built that way would diverge; every other mode takes the double
+ * reading, as the product does. */
+static float u_erf(float x) { return g_math == OR_MATH_LIBM_FLOAT ? erff(x) : (float)erf((double)x); }
+static float u_acos(float x) { return g_math == OR_MATH_LIBM_FLOAT ? acosf(x) : (float)acos((double)x); }
+static float u_exp_add(float r, float x)
+{
+    return g_math == OR_MATH_LIBM_FLOAT ? r + expf(x) : (float)((double)r + exp((double)x));
+}
 
 /* ---------------------------------------------------------------- vectors
  * madrona::math Vector3 / Quat semantics (operator order as written in the
@@ -557,7 +569,7 @@ static void sys_shot_pct(OWorld *w, OAgent *a) /* game.cpp:758-809 */
     float fstd = sqrtf((dstd * dstd / 3.f) + (defstd * defstd / 3.f) + (vstd * vstd / 3.f));
     float mma = m_atanf(K_HOOP_ZONE / dh);
     float z = mma / fstd;
-    a->shot_pct = (float)erf((double)(z / sqrtf(2.f)));
+    a->shot_pct = u_erf(z / sqrtf(2.f));
 }
 
 static void sys_score(OWorld *w, OHoop *h) /* game.cpp:873-953 */
@@ -792,7 +804,7 @@ static void sys_defense(OWorld *w, OAgent *a) /* game.cpp:651-755 */
     a->act[0] = 1;
     a->act[1] = best;
     V3 fv = qrot(a->q, FWD);
-    float ang = (float)acos((double)clampf_(vdot(fv, vnorm(mv)), -1.f, 1.f));
+    float ang = u_acos(clampf_(vdot(fv, vnorm(mv)), -1.f, 1.f));
     if (ang > K_PI / 8.f) {
         float cr = fv.x * mv.y - fv.y * mv.x;
         if (cr < 0.f) a->act[2] = -1;
@@ -921,7 +933,7 @@ static void sys_reward(OWorld *w, OAgent *a) /* game.cpp:811-870 */
         }
     } else {
         a->reward -= 1.f;
-        a->reward = (float)((double)a->reward + exp((double)(-0.4f * dist)));
+        a->reward = u_exp_add(a->reward, -0.4f * dist);
     }
 }
 

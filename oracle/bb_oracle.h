@@ -45,6 +45,8 @@ enum {
 /* math modes */
 #define OR_MATH_CR   0  /* float transcendental f(x) := (float) libm_double(x)  */
 #define OR_MATH_LIBM 1  /* literal glibc float calls, exactly as the reference */
+#define OR_MATH_LIBM_FLOAT 2  /* as LIBM, but game.cpp:746,808,868's unqualified acos / erf / exp bound
+                                 to the float overloads (acosf / erff / expf): the unpinned other reading */
 
 typedef struct oracle_cfg {
     int32_t num_agents;

@@ -32,6 +32,7 @@ FLAG_NO_TAG_MASK = 0x2
 FLAG_FULL_GAME = 0x4
 MATH_CR = 0
 MATH_LIBM = 1
+MATH_LIBM_FLOAT = 2  # the float-overload reading of game.cpp:746,808,868
 
 # Cumulative event counters (bb_oracle.h OR_EV_*), in enum order.
 EVENTS = [

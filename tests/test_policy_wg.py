@@ -40,12 +40,3 @@ def test_gpu_policy_wg_forced_equals_host():
                        timeout=240)
     assert r.returncode == 0 and "WG_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
-
-@pytest.mark.gpu
-def test_gpu_policy_rows_forced_equals_host():
-    """k_policy_rows (one row per lane, weights as scalar operands) forced on
-    at every row count: bit-identical to the host policy as well."""
-    env = dict(os.environ, MADRONA_BB_POLICY_ROWS="1", PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=240)
-    assert r.returncode == 0 and "WG_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
