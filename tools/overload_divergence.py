@@ -44,6 +44,7 @@ def world_masks(a: Oracle, b: Oracle):
     exact = np.zeros(W, bool)
     outside = np.zeros(W, bool)
     cols = []
+    maxdiff = {}
     for n in ALL_COLUMNS:
         x, y = a.export(n), b.export(n)
         d = (x.view(np.uint32) != y.view(np.uint32)).reshape(W, -1).any(axis=1)
@@ -56,7 +57,8 @@ def world_masks(a: Oracle, b: Oracle):
                 diff = np.abs(x.astype(np.float64) - y.astype(np.float64))
                 tol = FLOAT_ATOL + 1e-6 * np.abs(y.astype(np.float64))
                 outside |= (diff > tol).reshape(W, -1).any(axis=1)
-    return anyd, exact, outside, cols
+                maxdiff[n] = float(np.nanmax(diff))
+    return anyd, exact, outside, cols, maxdiff
 
 
 def run_case(name: str, c: dict, seed: int = 321) -> dict:
@@ -69,6 +71,7 @@ def run_case(name: str, c: dict, seed: int = 321) -> dict:
     first = None
     first_cols: list = []
     ever = np.zeros(W, bool)
+    maxabs: dict = {}
     checks = {}
     for t in range(steps):
         if c.get("sparse"):
@@ -86,7 +89,9 @@ def run_case(name: str, c: dict, seed: int = 321) -> dict:
             b.random_actions(seed, t)
         a.step()
         b.step()
-        anyd, exact, outside, cols = world_masks(a, b)
+        anyd, exact, outside, cols, md = world_masks(a, b)
+        for n, v in md.items():
+            maxabs[n] = max(maxabs.get(n, 0.0), v)
         ever |= anyd
         if first is None and anyd.any():
             first, first_cols = t + 1, cols
@@ -95,7 +100,7 @@ def run_case(name: str, c: dict, seed: int = 321) -> dict:
                              "worlds_outside_float_bar": float(outside.mean()), "columns": cols}
     return {"case": name, "worlds": W, "steps": steps, "flags": c.get("flags", {}),
             "first_diverging_step": first, "first_diverging_columns": first_cols,
-            "worlds_ever_diverged": float(ever.mean()), "checkpoints": checks}
+            "worlds_ever_diverged": float(ever.mean()), "max_abs_float_diff": maxabs, "checkpoints": checks}
 
 
 def main():
