@@ -402,17 +402,18 @@ def main():
             wall2 = time.perf_counter() - t0
             ev = sum(pol2.rollout(sim2, K2, b2, seed=args.seed, step0=(2 + rollouts + i) * K2, time_kernels=True)
                      for i in range(rollouts)) / rollouts
-            # algorithmic bytes per PPO step: the world step's B(2) plus per
-            # trainee row the policy's observation read (128 floats), the
-            # buffer.obs record, the action row into the action tensor and
-            # into buffer.actions, log-prob, value, and the reward / done read
-            # from the sim and recorded (ppo.py:129-134)
-            per_row = 4 * 128 * 2 + 24 * 2 + 4 * 2 + 8 * 2
-            step_bytes = W2 * (L0.bb_algorithmic_bytes_per_world(2) + per_row)
+            # algorithmic bytes per PPO step of the path this call takes
+            # (bb_rollout_policy_bytes): what that loop as built
+            # must move per call of K2 steps with every record, over K2
+            path = int(L0.bb_rollout_policy_path(sim2._h, 0, 0))
+            step_bytes = W2 * int(L0.bb_rollout_policy_bytes(sim2._h, 0, 0, K2)) / K2
             us_step = ev * 1e3 / K2
             line = {"worlds": W2, "agents": 2, "rollout": K2, "rollouts": rollouts,
                     "value": W2 * K2 * rollouts / wall2, "unit": "env-steps/s",
                     "us_per_step": wall2 * 1e6 / (K2 * rollouts), "rollout_avg_us_events": ev * 1e3,
+                    "path": {1: "k_rollout_policy (one launch per rollout)",
+                             2: "k_policy once, then k_step_ppo per step (the step + the next policy pass)",
+                             3: "k_policy + k_step per step"}.get(path, str(path)),
                     "roofline": {"bound": "hbm", "scope": "whole PPO step (policy pass + world step + records)",
                                  "algorithmic_bytes_per_step": step_bytes,
                                  "achieved": step_bytes / us_step / 1e3, "peak": HBM_PEAK_GBS, "unit": "GB/s",

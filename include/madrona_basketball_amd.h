@@ -242,12 +242,15 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
  * Sampling as bb_policy_forward with step = step0 + k (stochastic = 0: argmax);
  * the opponent samples with seed ^ 0x9E3779B9.  Equal, bit for bit, to n x
  * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
- * On gfx950 without an opponent (and up to 16 384 worlds) one fused launch
- * runs all n steps; flags BB_ROLLOUT_PER_STEP forces a policy launch and a
- * step launch per step instead.  From 32 768 worlds the per-step launches of
- * two world halves go to `stream` and to a second stream the simulator owns
- * (created on first use, destroyed by bb_destroy); `stream` waits for both
- * before the call's last work, so stream order holds for the caller.
+ * On gfx950 without an opponent, up to 16 384 worlds one fused launch runs
+ * all n steps (BB_PPO_PATH_FUSED_ROLLOUT); from 32 768 worlds a policy launch
+ * and then one launch per step that runs the step and the next policy pass
+ * (BB_PPO_PATH_FUSED_STEP).  flags BB_ROLLOUT_PER_STEP forces a policy launch
+ * and a step launch per step instead (so does an opponent); from 32 768
+ * worlds those per-step launches of two world halves go to `stream` and to a
+ * second stream the simulator owns (created on first use, destroyed by
+ * bb_destroy); `stream` waits for both before the call's last work, so stream
+ * order holds for the caller.
  * kernel_ms (CUDA mode): time from the first launch to the last, after a sync. */
 typedef struct bb_policy_rollout_buffers {
     float *obs;
@@ -257,6 +260,16 @@ typedef struct bb_policy_rollout_buffers {
 int bb_rollout_policy(bb_sim *sim, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
                       int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
                       const bb_policy_rollout_buffers *out, uint32_t flags, void *stream, float *kernel_ms);
+
+/* The implementation bb_rollout_policy takes on this simulator, and the
+ * algorithmic bytes of one call of n steps with every output recorded (the
+ * bytes that path must move: HBM roofline of the PPO loop). */
+#define BB_PPO_PATH_HOST 0          /* CPU mode: the host executor */
+#define BB_PPO_PATH_FUSED_ROLLOUT 1 /* one k_rollout_policy launch for all n steps */
+#define BB_PPO_PATH_FUSED_STEP 2    /* a policy launch, then one k_step_ppo per step */
+#define BB_PPO_PATH_PER_STEP 3      /* a policy launch and a step launch per step */
+int32_t bb_rollout_policy_path(const bb_sim *sim, int32_t with_opponent, uint32_t flags);
+int64_t bb_rollout_policy_bytes(const bb_sim *sim, int32_t with_opponent, uint32_t flags, int32_t n);
 
 int bb_set_action(bb_sim *sim, int32_t world_idx, int32_t agent_idx, int32_t move_speed,
                   int32_t move_angle, int32_t rotate, int32_t grab, int32_t pass,

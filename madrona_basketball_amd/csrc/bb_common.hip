@@ -353,6 +353,12 @@ hipError_t launch_rollout_policy(int n, const Params &p, const PolicyRolloutArgs
 #undef CALL
 }
 
+hipError_t launch_step_ppo_2(const Params &p, const PpoStepArgs &a, hipStream_t s);  // bb_kernels.hip (N = 2)
+hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s)
+{
+    return n == 2 ? launch_step_ppo_2(p, a, s) : hipErrorNotSupported;
+}
+
 bool fused_rollout_n(int n)
 {
     switch (n) {

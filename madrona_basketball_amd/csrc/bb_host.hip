@@ -998,6 +998,31 @@ static int64_t ppo_fused_max_worlds()
     return v;
 }
 
+// PPO's loop as one k_step_ppo launch per step (the trainee's policy pass fused
+// behind the world step, its rows read from LDS) from this many worlds on;
+// MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never).
+static int64_t ppo_step_fused_min_worlds()
+{
+    static const int64_t v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS");
+        return (int64_t)(e && *e ? std::atoll(e) : 32768);
+    }();
+    return v;
+}
+
+// The implementation bb_rollout_policy takes (BB_PPO_PATH_*).
+static int32_t ppo_path(const bb_sim *s, bool opponent, uint32_t flags)
+{
+    if (s->cfg.exec_mode != BB_EXEC_CUDA) return BB_PPO_PATH_HOST;
+    const int64_t W = s->cfg.num_worlds;
+    if (!(flags & BB_ROLLOUT_PER_STEP) && !opponent && bb::fused_rollout_n(s->n) && W <= ppo_fused_max_worlds())
+        return BB_PPO_PATH_FUSED_ROLLOUT;
+    if (!(flags & BB_ROLLOUT_PER_STEP) && !opponent && s->n == 2 && ppo_step_fused_min_worlds() > 0 &&
+        W >= ppo_step_fused_min_worlds())
+        return BB_PPO_PATH_FUSED_STEP;
+    return BB_PPO_PATH_PER_STEP;
+}
+
 int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_weights *opponent, int32_t n,
                       int32_t trainee, int32_t stochastic, uint32_t seed, uint32_t step0,
                       const bb_policy_rollout_buffers *out, uint32_t flags, void *stream, float *kernel_ms)
@@ -1075,8 +1100,8 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         if (!ev.create()) return fail(BB_ERR_HIP, "hipEventCreate");
         (void)hipEventRecord(ev.e0, st);
     }
-    const bool fused = !(flags & BB_ROLLOUT_PER_STEP) && !opponent && bb::fused_rollout_n(s->n) &&
-                       W <= ppo_fused_max_worlds();
+    const int32_t path = ppo_path(s, opponent != nullptr, flags);
+    const bool fused = path == BB_PPO_PATH_FUSED_ROLLOUT;
     if (fused) {
         bb::PolicyRolloutArgs r{};
         r.w = policy_weights(w);
@@ -1111,6 +1136,34 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             (void)hipFree(ts);
         }
     }
+    const bool step_fused = path == BB_PPO_PATH_FUSED_STEP;
+    if (step_fused) {
+        // policy pass 0 on the sim's rows, then per step k one k_step_ppo:
+        // step k, then policy pass k + 1 (or the value pass after the last step)
+        hipError_t e = bb::launch_policy(pass(0, false), st);
+        for (int32_t k = 0; k < n && e == hipSuccess; k++) {
+            bb::PpoStepArgs a{};
+            a.w = policy_weights(w);
+            a.trainee = trainee; a.stochastic = stochastic ? 1 : 0; a.seed = seed;
+            a.step = step0 + (uint32_t)(k + 1);
+            a.last = k + 1 == n ? 1 : 0;
+            if (out->reward) {
+                a.reward = out->reward + (int64_t)k * W;
+                a.done = out->done + (int64_t)k * W;
+            }
+            if (!a.last) {
+                const int64_t k1 = k + 1;
+                a.obs_rec = out->obs ? out->obs + k1 * W * bb::POL_IN : nullptr;
+                a.act_out = out->actions ? out->actions + k1 * W * 6 : nullptr;
+                a.log_prob = out->log_prob ? out->log_prob + k1 * W : nullptr;
+                a.value = out->value ? out->value + k1 * W : nullptr;
+            } else {
+                a.value = out->next_value;
+            }
+            e = bb::launch_step_ppo(s->n, s->p, a, st);
+        }
+        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy fused step launch");
+    }
     // one part (worlds [w0, w0 + cnt)) of policy pass k (or of the opponent's)
     const auto part_pass = [&](bb::PolicyArgs a, int64_t w0, int64_t cnt, const bb::Params &sp) {
         const auto adv = [&](auto *&ptr, int64_t per) {
@@ -1133,7 +1186,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         a.mt = ppo_split_mt();  // k_policy<2>: 276 registers, a policy wave fits beside a step wave on one SIMD
         return a;
     };
-    const bool split = !fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
+    const bool split = !fused && !step_fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
     // steps 0 .. n-2 write the trainee's rows into buffer.obs[k + 1] only (the
     // sim's copy of them is read by nobody before the last step rewrites
     // every row); the next policy pass reads them there
@@ -1167,7 +1220,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
     // k >= 1 reads its rows without recording them: from the policy's
     // registers the record took 9 us of a 61.6 us step at 65 536 worlds
     // (each store instruction touching 64 rows' lines; profiles/r04/h_*)
-    for (int32_t k = 0; k < (fused ? 0 : n); k++) {
+    for (int32_t k = 0; k < ((fused || step_fused) ? 0 : n); k++) {
         for (int h = 0; h < parts; h++) {
             bb::PolicyArgs a = pass(k, false);
             if (k > 0) a.obs_out = nullptr;
@@ -1212,7 +1265,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[MP + h], 0);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy join");
     }
-    if (final_needed && !fused && !split) {
+    if (final_needed && !fused && !split && !step_fused) {
         hipError_t e = bb::launch_policy(pass(n, true), st);
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
     }
@@ -1455,6 +1508,43 @@ int64_t bb_rollout_state_bytes_per_world(int32_t n)
     // once per launch: the B(N) state columns except the per-step action read
     // and observation write (loaded at the start, stored after the last step)
     return bb_algorithmic_bytes_per_world(n) - (int64_t)n * (24 + 4 * (int64_t)bb::obs_used(n));
+}
+
+int32_t bb_rollout_policy_path(const bb_sim *s, int32_t with_opponent, uint32_t flags)
+{
+    if (!s) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy_path: sim");
+    return ppo_path(s, with_opponent != 0, flags);
+}
+
+int64_t bb_rollout_policy_bytes(const bb_sim *s, int32_t with_opponent, uint32_t flags, int32_t n)
+{
+    if (!s || n < 1 || s->n != 2) return 0;
+    const int64_t B = bb_algorithmic_bytes_per_world(2);
+    const int64_t row = 4 * (int64_t)bb::obs_used(2);   // a sim observation row's values (412 B)
+    const int64_t rec = 4 * (int64_t)bb::POL_IN;        // a buffer.obs row (128 floats)
+    const int64_t outs = 24 + 4 + 4;                    // buffer.actions, log_probs, values
+    const int64_t rd = 4 + 4;                           // buffer.rewards, not_dones
+    // the first policy pass: the trainee's sim row in, buffer.obs[0], the
+    // action row into the sim, the outputs; the value pass: next_value
+    const int64_t pass0 = rec + rec + 24 + outs;
+    switch (ppo_path(s, with_opponent != 0, flags)) {
+    case BB_PPO_PATH_FUSED_ROLLOUT:
+        // state in once and out once (every row of the last step included); per
+        // step the policy's records and the step's reward / done
+        return B + (int64_t)n * (rec + outs + rd) + 4;
+    case BB_PPO_PATH_FUSED_STEP:
+        // steps 0..n-2: the world step without the trainee's sim row, its row
+        // into buffer.obs[k+1], the action row into the sim, the outputs, the
+        // reward / done; the last step: the whole world step, reward / done,
+        // next_value
+        return pass0 + (int64_t)(n - 1) * (B - row + rec + 24 + outs + rd) + B + rd + 4;
+    default:
+        // per step: the world step (the trainee's row into buffer.obs[k+1]
+        // instead of the sim from step 0 to n-2), then a policy pass reading
+        // that row back, the outputs, the reward / done read from the sim and
+        // recorded; then the value pass reads the last rows
+        return pass0 + (int64_t)(n - 1) * (B - row + rec + rec + 24 + outs + rd + rd) + B + rd + rd + rec + 4;
+    }
 }
 
 const char *bb_last_error(void) { return g_err.c_str(); }

@@ -1203,6 +1203,282 @@ __global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), 1) void k_rollout_policy(c
     }
 }
 
+// ------------------------------------------------------------------ PPO step
+// k_step_ppo<2>: one step of PPO's rollout loop with the trainee's policy pass
+// fused behind it (bb_rollout_policy from 32 768 worlds; scripts/ppo.py:65-134
+// over scripts/env.py:126-170).  A wave steps its 32 worlds exactly as
+// k_step<2> does (agent lanes, the world in registers), then the policy of
+// step k + 1 runs on the trainee's rows while they are in LDS: no second
+// launch, and the 512 bytes of each trainee row are never read back from HBM.
+//
+// Row passes split by the policy's layer-1 chain order.  Layer 1 is the
+// k-ordered MFMA chain of policy_layers: step j (0..31) feeds lane group q with
+// observation float 32q + j.  Pass P of the rows holds the floats with
+// ((i >> 4) & 1) == P -- for every q the steps j = 16P .. 16P + 15 -- at tile
+// slot (i >> 5) * 16 + (i & 15): pass 0 slots 0..55 (floats 96..103 of q = 3
+// included; 104..127 are the row's zero tail), pass 1 slots 0..47.  After a
+// pass is in the tile, the wave runs that pass's 16 chain steps for its two
+// 16-row M-tiles of trainee rows (the same operands in the same order as
+// every other policy kernel: bit-identical), then stores the pass's pieces.
+// The network's weights sit in LDS once per workgroup of WPG waves
+// (PolicyLdsWeights, 32.6 KB); each wave's tile (64 rows x 60 floats, 15 KB)
+// takes the LayerNorm / bucket-pass exchanges after the last pass.
+constexpr int PPS_RS = 60;  // tile row stride (floats): 14 pieces + 1, == 4 mod 8 dwords
+constexpr int PPS_TILE = WAVE * PPS_RS;
+
+template <int WPG>
+struct PpoStepLds {
+    PolicyLdsWeights wt;
+    float tile[WPG][PPS_TILE];
+};
+
+// Floats of pass P of a row into its tile row (compile-time indices: straight
+// float4 LDS writes of the pass's pieces, the other floats never computed).
+template <int P>
+struct PassSink {
+    float *row;
+    float b0, b1, b2, b3;
+    int idx;
+    __device__ void put(float v)
+    {
+        if (((idx >> 4) & 1) == P && idx < 4 * PhasedTile<2>::QU) {
+            switch (idx & 3) {
+            case 0: b0 = v; break;
+            case 1: b1 = v; break;
+            case 2: b2 = v; break;
+            default: *(float4 *)(row + ((idx >> 5) << 4) + (idx & 12)) = make_float4(b0, b1, b2, v); break;
+            }
+        }
+        idx++;
+    }
+    __device__ void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    __device__ void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+    __device__ void finish() { while (idx & 3) put(0.f); }
+};
+// The same for the rows of non-canonical team layouts (runtime indices).
+template <int P>
+struct PassSlowSink {
+    float *row;
+    int idx;
+    __device__ void put(float v)
+    {
+        if (idx < 4 * PhasedTile<2>::QU && ((idx >> 4) & 1) == P) row[((idx >> 5) << 4) + (idx & 15)] = v;
+        idx++;
+    }
+    __device__ void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    __device__ void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+};
+
+// Layer-1 chain steps 16P .. 16P + 15 of the wave's two M-tiles of trainee
+// rows (row m = 16 mt + c is world w0 + m; its tile row 2m + trainee).
+template <int P>
+__device__ __forceinline__ void ppo_layer1_pass(const float *tile, const PolicyLdsWeights &L, f32x4 (&acc)[2][2],
+                                                int trainee, int c, int q)
+{
+    constexpr int QD = P == 0 ? 2 : 0;  // float4 groups of lane group q = 3 holding row values
+    const int ng = q < 3 ? 4 : QD;
+    const float *r0 = tile + (2 * c + trainee) * PPS_RS + 16 * q;
+    const float *r1 = r0 + 32 * PPS_RS;
+#pragma unroll
+    for (int v = 0; v < 4; v++) {
+        const float4 m4 = *(const float4 *)&L.norm[0][32 * q + 16 * P + 4 * v];
+        const float4 i4 = *(const float4 *)&L.norm[1][32 * q + 16 * P + 4 * v];
+        const float4 b0 = *(const float4 *)&L.w1[q][c][16 * P + 4 * v];
+        const float4 b1 = *(const float4 *)&L.w1[q][16 + c][16 * P + 4 * v];
+        // lanes past their row values read their row's first piece (a valid
+        // address) and feed the zero tail
+        const bool has = v < ng;
+        const int o = has ? 4 * v : 0;
+        float4 x0 = *(const float4 *)(r0 + o), x1 = *(const float4 *)(r1 + o);
+        if (!has) x0 = x1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        const float nm[4] = {m4.x, m4.y, m4.z, m4.w}, ni[4] = {i4.x, i4.y, i4.z, i4.w};
+        const float w0[4] = {b0.x, b0.y, b0.z, b0.w}, w1[4] = {b1.x, b1.y, b1.z, b1.w};
+        const float xa[4] = {x0.x, x0.y, x0.z, x0.w}, xb[4] = {x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const float ya = pol_clamp((xa[e] - nm[e]) * ni[e]);
+            const float yb = pol_clamp((xb[e] - nm[e]) * ni[e]);
+            acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya, w0[e], acc[0][0], 0, 0, 0);
+            acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(ya, w1[e], acc[0][1], 0, 0, 0);
+            acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(yb, w0[e], acc[1][0], 0, 0, 0);
+            acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(yb, w1[e], acc[1][1], 0, 0, 0);
+        }
+    }
+}
+
+// Stores of pass P: tile piece t of row r is row piece 8 (t >> 2) + 4P + (t & 3).
+// Sim rows (the non-trainee's; every row when ALL): the pass's NS pieces of
+// the 64 rows.  Record rows (buffer.obs, the trainee's): 16 pieces per pass,
+// the zero tail included, at rec + m * 512.  Rows of worlds past the grid's
+// end (bit clear in `live`) store nothing.
+template <int P, bool ALL>
+__device__ __forceinline__ void ppo_flush_pass(const float *tile, char *obs, char *rec, uint64_t live, int trainee,
+                                               int lane)
+{
+    constexpr int NS = P == 0 ? 14 : 12;
+    constexpr int NR = ALL ? WAVE : WAVE / 2;  // sim rows stored
+    constexpr int SIT = NR * NS / WAVE;        // store instructions (14 / 12 or 7 / 6)
+    static_assert(NR * NS % WAVE == 0, "whole store instructions");
+    constexpr int OWB = 128 * 4;
+    {
+        vf4 v[SIT];
+        uint32_t off[SIT];
+        bool ok[SIT];
+#pragma unroll
+        for (int i = 0; i < SIT; i++) {
+            const int f = i * WAVE + lane, rr = f / NS, t = f - rr * NS;
+            const int r = ALL ? rr : 2 * rr + (1 - trainee);
+            ok[i] = (live >> r) & 1ull;
+            off[i] = (uint32_t)(r * OWB + (8 * (t >> 2) + 4 * P + (t & 3)) * 16);
+            v[i] = *(const vf4 *)(tile + r * PPS_RS + 4 * t);
+        }
+#pragma unroll
+        for (int i = 0; i < SIT; i++)
+            if (ok[i]) row_store<BB_STEP_AUX>(obs, off[i], v[i]);
+    }
+    if (rec) {  // wave-uniform
+        constexpr int RIT = (WAVE / 2) * 16 / WAVE;  // 8
+        vf4 v[RIT];
+        uint32_t off[RIT];
+        bool ok[RIT];
+#pragma unroll
+        for (int i = 0; i < RIT; i++) {
+            const int f = i * WAVE + lane, m = f >> 4, t = f & 15;
+            const int r = 2 * m + trainee;
+            ok[i] = (live >> r) & 1ull;
+            off[i] = (uint32_t)(m * OWB + (8 * (t >> 2) + 4 * P + (t & 3)) * 16);
+            v[i] = t < NS ? *(const vf4 *)(tile + r * PPS_RS + 4 * t) : vf4{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int i = 0; i < RIT; i++)
+            if (ok[i]) row_store<BB_REC_AUX>(rec, off[i], v[i]);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void ppo_emit_pass(const World<2> &v, const Ctx &c, const SharedObs<2> &sh, bool active,
+                                              bool fast, bool share, float *trow, int32_t ib)
+{
+    if (!active) return;
+    if (fast) {
+        PassSink<P> o;
+        o.row = trow; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+        if (share) emit_row_shared(v, c, sh, 0, o, ib);
+        else emit_row_fast(v, c, 0, o, ib);
+    } else {
+        PassSlowSink<P> o;
+        o.row = trow; o.idx = 0;
+        emit_row_slow(v, c, 0, o, ib);
+    }
+}
+
+template <int WPG, bool LAST>
+__device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs &a, PpoStepLds<WPG> &S, int wave,
+                                              int lane)
+{
+    constexpr int N = 2;
+    float *tile = S.tile[wave];
+    const int k = lane % N;
+    const int64_t w0 = ((int64_t)blockIdx.x * WPG + wave) * (WAVE / N);
+    const int64_t w = w0 + lane / N;
+    const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
+    const int trainee = a.trainee;
+    const LaneAgents<N, MODE_FULL> ag{k, &p};
+
+    World<N> s;
+    Ctx c = make_ctx(p, w, k == 0);
+    World<N> v;
+    if (active) {
+        load_world(s, p, w);
+        {
+            Orig<N> o;
+            capture(o, s);
+            LaneOrig x;
+            x.world = world_orig(o);
+            x.agent = pick_by<N>(k, [&](int j) { return o.ag[j]; });
+            park_words(tile, lane, x);
+        }
+    }
+    // the workgroup's copy of the network (read after the barrier below)
+    policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
+    if (active) step_world_pre_obs(s, c, ag);
+    if (active) {
+        agent_view(s, v, k);
+        sys_reward_agent(v, 0, AGENT0_ID + k);
+        const LaneOrig x = unpark_words<LaneOrig>(tile, lane);
+        store_world_agent<N, BB_COL_AUX>(v, p, w * N + k, 0, &x.agent);
+        if (k == 0) {
+            Orig<N> o;
+            set_world_orig(o, x.world);
+            store_world_shared<N, BB_COL_AUX>(s, p, w, &o);
+        }
+        if (k == trainee && a.reward) {  // buffer.rewards / not_dones source of step k
+            a.reward[w] = v.rew[0];
+            a.done[w] = v.done[0];
+        }
+    }
+    const int32_t ib = active ? inbounder_id(s) : -1;
+    const bool share = active && obs_sharable(s);
+    SharedObs<N> sh;
+    lane_shared_obs(v, c, active, sh);
+    const bool fast = active && canonical_slots(v, 0);
+    const uint64_t live = __ballot(active);
+    char *obs = (char *)(p.c.obs + w0 * N * (int64_t)obs_width(N));                // wave-uniform
+    char *rec = (!LAST && a.obs_rec) ? (char *)(a.obs_rec + w0 * (int64_t)POL_IN) : nullptr;
+    const int pl = lane & 15, pq = lane >> 4;
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    wave_sync();  // the parked words are read
+    ppo_emit_pass<0>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
+    lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
+    ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
+    ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
+    wave_sync();
+    ppo_emit_pass<1>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
+    wave_sync();
+    ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
+    ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
+    wave_sync();
+    if (LAST && !a.value) return;  // (wave-uniform; no barrier follows)
+    // LayerNorm 1, layer 2, heads (the tile's first 32 x 33 floats), then the
+    // bucket pass (its exchange right behind them)
+    float (*lt)[33] = (float (*)[33])tile;
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++)
+        ln_relu_to_tile(acc[mt][0], acc[mt][1], S.wt.cst[0][pl], S.wt.cst[0][pl + 16], S.wt.cst[1][pl],
+                        S.wt.cst[1][pl + 16], S.wt.cst[2][pl], S.wt.cst[2][pl + 16], lt + 16 * mt, pl, pq);
+    pol_wave_sync();
+#pragma unroll
+    for (int mt = 0; mt < 2; mt++) policy_tail_lds(S.wt, lt + 16 * mt, pl, pq);
+    if constexpr (LAST) {
+        if (a.value && lane < 32 && w0 + lane < p.num_worlds) a.value[w0 + lane] = lt[lane][POL_LOGITS];
+    } else {
+        PolicyArgs pa{};
+        pa.rows = p.num_worlds;
+        pa.stochastic = a.stochastic;
+        pa.seed = a.seed;
+        pa.step = a.step;
+        pa.actions = p.c.action + trainee * 6;
+        pa.act_stride = N * 6;
+        pa.act_out = a.act_out;
+        pa.log_prob = a.log_prob;
+        pa.value = a.value;
+        BucketLds<32> &bl = *(BucketLds<32> *)(tile + 32 * 33);
+        bucket_pass_spread<32>(pa, lt, w0, lane, bl);
+    }
+}
+
+template <int WPG, bool LAST>
+__global__ __launch_bounds__(WAVE * WPG, 2) void k_step_ppo(const Params p, const PpoStepArgs a)
+{
+    if constexpr (BB_N == 2) {
+        __shared__ PpoStepLds<WPG> S;
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        ppo_step_wave<WPG, LAST>(p, a, S, wave, (int)threadIdx.x % WAVE);
+    }
+}
+
 // ------------------------------------------------------------------ N >= 4
 // One lane per agent; the world's state lives in LDS and its N lanes run the
 // world-level systems on it together (same instructions, same values); the
@@ -1955,6 +2231,27 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
         return hipGetLastError();
     }
 }
+
+#if BB_N == 2
+// k_step_ppo: 8-wave workgroups (the weights' 32.6 KB shared by 256 worlds,
+// 155 KB of LDS: one workgroup and 2 waves per SIMD per CU) while the grid
+// fills the device with them, 4-wave workgroups below that.
+hipError_t launch_step_ppo_2(const Params &p, const PpoStepArgs &a, hipStream_t s)
+{
+    const int64_t waves = (p.num_worlds + WAVE / 2 - 1) / (WAVE / 2);
+    const bool big = waves >= 8 * (int64_t)device_cus();
+    const int wpg = big ? 8 : 4;
+    const dim3 grid((unsigned)((waves + wpg - 1) / wpg)), block(WAVE * wpg);
+    if (big) {
+        if (a.last) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step_ppo<8, true>), grid, block, 0, s, p, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step_ppo<8, false>), grid, block, 0, s, p, a);
+    } else {
+        if (a.last) hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step_ppo<4, true>), grid, block, 0, s, p, a);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_step_ppo<4, false>), grid, block, 0, s, p, a);
+    }
+    return hipGetLastError();
+}
+#endif
 
 template <int N>
 hipError_t launch_init_t(const Params &p, hipStream_t s)

@@ -45,6 +45,26 @@ struct PolicyRolloutArgs {
     uint64_t *diag_ts;    // diagnostics only: per-step phase clocks of workgroup 0 ([steps][4])
 };
 
+// One step of PPO's rollout loop with the policy fused behind it
+// (k_step_ppo<2>, bb_rollout_policy from 32 768 worlds): step k on the
+// trainee's actions already in the sim's action column, then the policy on the
+// trainee's rows after the step (scripts/ppo.py:65-134 over env.py:126-170) --
+// the actions of step k + 1 into the action column, buffer.obs/actions/
+// log_probs/values[k + 1] -- or, after the rollout's last step, the value only
+// (next_value, ppo.py:136-137).  All output pointers optional.
+struct PpoStepArgs {
+    PolicyWeights w;
+    float *reward, *done;       // [W] buffer.rewards / not_dones source of step k (the trainee's)
+    float *obs_rec;             // [W][128] buffer.obs[k + 1] (not on the last step)
+    int32_t *act_out;           // [W][6]   buffer.actions[k + 1]
+    float *log_prob, *value;    // [W]      buffer.log_probs / values[k + 1], or next_value on the last step
+    int32_t trainee, stochastic;
+    int32_t last;               // the rollout's last step: every row into the sim's obs, value only
+    uint32_t seed, step;        // the policy's sampling key (seed, step0 + k + 1)
+};
+// N = 2 only (hipErrorNotSupported otherwise)
+hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s);
+
 // Trajectory recorder (bb_record): NSEG column segments per recorded world.
 constexpr int RECORD_SEGS = 10;
 struct RecordArgs {

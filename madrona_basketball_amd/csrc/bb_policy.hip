@@ -169,21 +169,13 @@ __global__ __launch_bounds__(64) void k_policy(const PolicyArgs a)
 // in the same order, the same LayerNorm and bucket pass), so the outputs are
 // bit-identical.
 //
-// LDS images of the weights, conflict-free for the lanes' 16-byte reads
-// (lane (c, q) reads W[16t + c][k-chunk q]): planes [q][n][j] padded to 36 /
-// 12 floats (tools-free check: every ds_read_b128 lane group of 16 lanes
-// covers the 64 banks once).
+// The weights' LDS images: PolicyLdsWeights (bb_policy_dev.h).
 #ifndef BB_PWG_WAVES
 #define BB_PWG_WAVES 12  // 3 per SIMD: 141-159 VGPRs (at 16 the 128-VGPR budget spills 16-104 B)
 #endif
 constexpr int PWG_WAVES = BB_PWG_WAVES;
-constexpr int PWG_P1 = 36, PWG_P2 = 12;
 struct PolicyWgLds {
-    float w1[4][32][PWG_P1];  // W1[n][32q + j]
-    float w2[4][32][PWG_P2];  // W2[n][8q + j]
-    float wh[4][32][PWG_P2];  // head_w[n][8q + j]
-    float norm[2][POL_IN];
-    float cst[7][32];  // b1, ln1_w, ln1_b, b2, ln2_w, ln2_b, head_b (read at their use: no live registers)
+    PolicyLdsWeights wt;
     float tile[PWG_WAVES][16][33];
     BucketLds<16> bl[PWG_WAVES];
 };
@@ -216,23 +208,7 @@ __global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a
     // the first tile's rows in flight under the weight copy
     float xn[32];
     if (tw0 < tiles) load_rows(tw0 * 16, xn);
-    for (int i = tid; i < 32 * 32; i += (int)blockDim.x) {  // W1 [32][128] as float4
-        const int n = i >> 5, k = 4 * (i & 31);
-        *(float4 *)&L.w1[k >> 5][n][k & 31] = ((const float4 *)W.w1)[i];
-    }
-    for (int i = tid; i < 32 * 8; i += (int)blockDim.x) {  // W2, head_w [32][32] as float4
-        const int n = i >> 3, k = 4 * (i & 7);
-        *(float4 *)&L.w2[k >> 3][n][k & 7] = ((const float4 *)W.w2)[i];
-        *(float4 *)&L.wh[k >> 3][n][k & 7] = ((const float4 *)W.head_w)[i];
-    }
-    for (int k = tid; k < POL_IN; k += (int)blockDim.x) {
-        L.norm[0][k] = W.obs_mean[k];
-        L.norm[1][k] = W.obs_inv[k];
-    }
-    for (int k = tid; k < 7 * 32; k += (int)blockDim.x) {
-        const float *src[7] = {W.b1, W.ln1_w, W.ln1_b, W.b2, W.ln2_w, W.ln2_b, W.head_b};
-        L.cst[k >> 5][k & 31] = src[k >> 5][k & 31];
-    }
+    policy_weights_to_lds(L.wt, W, tid, (int)blockDim.x);
     __syncthreads();
     pol_trace_wg(a, tw0, 1, true);
     float (*tile)[33] = L.tile[wave];
@@ -257,11 +233,11 @@ __global__ __launch_bounds__(64 * PWG_WAVES) void k_policy_wg(const PolicyArgs a
         // inside the loop instead of being hoisted into 128 live registers
         int z = 0;
         __asm__ volatile("" : "+v"(z));
-        const float (*nrm)[POL_IN] = (const float (*)[POL_IN])(&L.norm[0][0] + z);
-        const float (*w1l)[32][PWG_P1] = (const float (*)[32][PWG_P1])(&L.w1[0][0][0] + z);
-        const float (*w2l)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.w2[0][0][0] + z);
-        const float (*whl)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.wh[0][0][0] + z);
-        const float (*cs)[32] = (const float (*)[32])(&L.cst[0][0] + z);
+        const float (*nrm)[POL_IN] = (const float (*)[POL_IN])(&L.wt.norm[0][0] + z);
+        const float (*w1l)[32][PWG_P1] = (const float (*)[32][PWG_P1])(&L.wt.w1[0][0][0] + z);
+        const float (*w2l)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.wt.w2[0][0][0] + z);
+        const float (*whl)[32][PWG_P2] = (const float (*)[32][PWG_P2])(&L.wt.wh[0][0][0] + z);
+        const float (*cs)[32] = (const float (*)[32])(&L.wt.cst[0][0] + z);
         // layer 1: normalisation, then the two accumulator chains (policy_layers).
         // The LDS operands are read one 4-float group ahead of their use and the
         // groups fenced with scheduling barriers: hoisted all at once they would

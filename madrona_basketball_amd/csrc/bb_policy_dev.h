@@ -321,6 +321,83 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     bucket_stamp(ts, 3, lane);
 }
 
+// The network's weights in LDS, shared by the waves of a workgroup (k_policy_wg,
+// k_step_ppo): images conflict-free for the lanes' 16-byte reads (lane (c, q)
+// reads W[16t + c][k-chunk q]): planes [q][n][j] padded to 36 / 12 floats
+// (every ds_read_b128 lane group of 16 lanes covers the 64 banks once).
+constexpr int PWG_P1 = 36, PWG_P2 = 12;
+struct PolicyLdsWeights {
+    float w1[4][32][PWG_P1];  // W1[n][32q + j]
+    float w2[4][32][PWG_P2];  // W2[n][8q + j]
+    float wh[4][32][PWG_P2];  // head_w[n][8q + j]
+    float norm[2][POL_IN];    // obs_mean, obs_inv
+    float cst[7][32];         // b1, ln1_w, ln1_b, b2, ln2_w, ln2_b, head_b
+};
+
+// Thread tid of nt copies its share of the weights into L (the caller orders
+// the writes before their first read with a workgroup barrier).
+__device__ __forceinline__ void policy_weights_to_lds(PolicyLdsWeights &L, const PolicyWeights &W, int tid, int nt)
+{
+    for (int i = tid; i < 32 * 32; i += nt) {  // W1 [32][128] as float4
+        const int n = i >> 5, k = 4 * (i & 31);
+        *(float4 *)&L.w1[k >> 5][n][k & 31] = ((const float4 *)W.w1)[i];
+    }
+    for (int i = tid; i < 32 * 8; i += nt) {  // W2, head_w [32][32] as float4
+        const int n = i >> 3, k = 4 * (i & 7);
+        *(float4 *)&L.w2[k >> 3][n][k & 7] = ((const float4 *)W.w2)[i];
+        *(float4 *)&L.wh[k >> 3][n][k & 7] = ((const float4 *)W.head_w)[i];
+    }
+    for (int k = tid; k < POL_IN; k += nt) {
+        L.norm[0][k] = W.obs_mean[k];
+        L.norm[1][k] = W.obs_inv[k];
+    }
+    for (int k = tid; k < 7 * 32; k += nt) {
+        const float *src[7] = {W.b1, W.ln1_w, W.ln1_b, W.b2, W.ln2_w, W.ln2_b, W.head_b};
+        L.cst[k >> 5][k & 31] = src[k >> 5][k & 31];
+    }
+}
+
+// Layer 2 + LayerNorm + ReLU, then the heads, of one 16-row M-tile whose
+// layer-1 output is in tm[16][33], with the weights in LDS: row r's 19 logits
+// and value into tm[r][0..19].  The same operands in the same order as
+// policy_layers' second loop (lane (c, q): k = 8q + j).
+__device__ __forceinline__ void policy_tail_lds(const PolicyLdsWeights &L, float (*tm)[33], int c, int q)
+{
+#pragma unroll
+    for (int layer = 0; layer < 2; layer++) {
+        const float (*wl)[32][PWG_P2] = layer == 0 ? L.w2 : L.wh;
+        float h[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
+        pol_wave_sync();
+        float w0[8], w1[8];
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const float4 u0 = *(const float4 *)&wl[q][c][4 * v];
+            const float4 u1 = *(const float4 *)&wl[q][16 + c][4 * v];
+            w0[4 * v] = u0.x; w0[4 * v + 1] = u0.y; w0[4 * v + 2] = u0.z; w0[4 * v + 3] = u0.w;
+            w1[4 * v] = u1.x; w1[4 * v + 1] = u1.y; w1[4 * v + 2] = u1.z; w1[4 * v + 3] = u1.w;
+        }
+        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w0[j], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], w1[j], a1, 0, 0, 0);
+        }
+        if (layer == 0) {
+            ln_relu_to_tile(a0, a1, L.cst[3][c], L.cst[3][c + 16], L.cst[4][c], L.cst[4][c + 16], L.cst[5][c],
+                            L.cst[5][c + 16], tm, c, q);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                tm[4 * q + i][c] = a0[i] + L.cst[6][c];
+                tm[4 * q + i][c + 16] = a1[i] + L.cst[6][c + 16];
+            }
+        }
+        pol_wave_sync();
+    }
+}
+
 // The B operands and the per-column constants of one lane, loaded once per
 // wave and kept in registers for every tile it processes.
 struct PolicyRegs {

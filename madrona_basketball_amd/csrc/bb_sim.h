@@ -1740,11 +1740,9 @@ BB_HD void emit_row_view(const World<N> &s, const Ctx &c, int a, IntrOf intr, bo
     o.finish();
 }
 
-template <int N>
-BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
+template <int N, class Sink>
+BB_HD void emit_row_slow(const World<N> &s, const Ctx &c, int a, Sink &o, int32_t ib)
 {
-    SlowRowSink o;
-    o.row = row; o.idx = 0;
     F3 att, dfn;
     obs_header(s, c, o, a, &att, &dfn);
     const F3 p = s.pos(a);
@@ -1763,6 +1761,14 @@ BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == s.holder ? 1.f : 0.f);
     for (int j = 0; j < N; j++) o.put(AGENT0_ID + j == ib ? 1.f : 0.f);
     for (; o.idx < obs_width(N); ) o.put(0.f);
+}
+
+template <int N>
+BB_HD void fill_obs_slow(const World<N> &s, const Ctx &c, int a, float *row, int32_t ib)
+{
+    SlowRowSink o;
+    o.row = row; o.idx = 0;
+    emit_row_slow(s, c, a, o, ib);
 }
 
 template <int N>
