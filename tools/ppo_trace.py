@@ -38,26 +38,39 @@ def main():
     wgs = [l for l in lines if l.startswith("wg")]
     G = (a.worlds + 31) // 32
     rows = np.array([[int(x) for x in l.split()] for l in steps[-a.steps:]], dtype=np.int64)
-    # the first policy wave's pass for step k (points 4..12): obs_out record,
-    # X into registers, layer 1 + its barrier, LayerNorm 1, layer 2, LayerNorm
-    # 2, heads, bucket pass
-    P = rows[:, 5:17]
-    names = ["(start)", "X -> registers", "layer 1 MFMA", "LN 1 (+bar)", "layer 2 MFMA (+bar)",
-             "LN 2 (+bar)", "heads (+bar)", "bucket maxima", "bucket per-logit", "bucket per-bucket",
-             "bucket outputs"]
-    sub = {n: [int(np.percentile((P[:, i + 1] - P[:, i]) * 10, q)) for q in (0, 50, 100)] for i, n in enumerate(names)}
-    wg = np.array([[int(x) for x in l.split()[1:]] for l in wgs[-G:]], dtype=np.int64)
-    t = rows[:, 1:5]
-    d_sys = (t[:, 1] - t[:, 0]) * 10
-    d_obs = (t[:, 2] - t[:, 1]) * 10
-    d_pol = (t[1:, 3] - t[:-1, 2]) * 10  # policy for step k+1 after the rows of step k
-    step = (t[1:, 0] - t[:-1, 0]) * 10
+    T = rows[:, 1:]  # clock points of each step (PPO_TRACE_POINTS, bb_kernels.hip)
     pct = lambda x: [int(np.percentile(x, q)) for q in (0, 50, 100)]
-    print(f"worlds {a.worlds}: ns per step {pct(step)}; S systems {pct(d_sys)}; S X free + rows {pct(d_obs)}; "
-          f"P policy {pct(d_pol)}; barrier hand-offs {pct(step[:] - d_sys[1:] - d_obs[1:] - d_pol)}")
-    wait = (P[1:, 0] - t[:-1, 2]) * 10  # S's rows done -> P's pass starts
-    print(f"  P pass ns (min, median, max): rows ready -> P start {pct(wait)}; "
-          + "; ".join(f"{n} {v}" for n, v in sub.items()))
+    if T.shape[1] == 16:  # the round-4 kernel (one hand-off of the rows): its layout
+        old = [(5, 6, "X -> registers"), (6, 7, "layer 1 MFMA"), (7, 8, "LN 1 (+bar)"), (8, 9, "layer 2 (+bar)"),
+               (9, 10, "LN 2 (+bar)"), (10, 11, "heads (+bar)"), (11, 12, "bucket maxima"),
+               (12, 13, "bucket per-logit"), (13, 14, "bucket per-bucket"), (14, 15, "bucket outputs"),
+               (15, 3, "to actions")]
+        step = (T[1:, 0] - T[:-1, 0]) * 10
+        print(f"worlds {a.worlds} (round-4 layout): ns per step {pct(step)}; S systems {pct((T[:, 1] - T[:, 0]) * 10)}; "
+              f"S X free + rows {pct((T[:, 2] - T[:, 1]) * 10)}; P {pct((T[1:, 3] - T[:-1, 2]) * 10)}")
+        print("  P: " + "; ".join(f"{n} {pct((T[1:, j] - T[1:, i]) * 10)}" for i, j, n in old))
+        return
+    ns = lambda i, j, sl=slice(None): (T[sl, j] - T[sl, i]) * 10
+    # S (sim wave): 0 actions in, 1 systems done, 20 row sources done, 21 pass 0
+    # of X written, 2 rows complete
+    step = (T[1:, 0] - T[:-1, 0]) * 10
+    print(f"worlds {a.worlds}: ns per step {pct(step)}")
+    print(f"  S: systems {pct(ns(0, 1))}; row sources {pct(ns(1, 20))}; X free + pass 0 {pct(ns(20, 21))}; "
+          f"pass 1 (+ last-step rows) {pct(ns(21, 2))}")
+    # P (first policy wave), pass of step k + 1 against S's rows of step k
+    names = [(4, 6, "layer 1, steps 0-15"), (6, 7, "wait: rows' second half"), (7, 8, "layer 1, steps 16-31 (+bar)"),
+             (8, 9, "LN 1 (+bar)"), (9, 10, "layer 2 (+bar)"), (10, 11, "LN 2 (+bar)"), (11, 12, "heads (+bar)"),
+             (12, 13, "bucket maxima"), (13, 14, "bucket per-logit"), (14, 15, "bucket per-bucket"),
+             (15, 16, "bucket outputs"), (16, 3, "to actions")]
+    print("  P: " + "; ".join(f"{n} {pct(ns(i, j, slice(1, None)))}" for i, j, n in names))
+    # the overlap: P's layer 1 on pass 0 of step k's rows starts before S has
+    # finished pass 1 of them
+    lead = (T[:-1, 2] - T[1:, 4]) * 10
+    print(f"  overlap: P starts layer 1 this many ns before S's rows are complete {pct(lead)}; "
+          f"P pass (start -> actions) {pct((T[1:, 3] - T[1:, 4]) * 10)}; "
+          f"S (actions in -> rows complete) {pct(ns(0, 2))}")
+    wg = np.array([[int(x) for x in l.split()[1:]] for l in wgs[-G:]], dtype=np.int64)
+    t = T[:, [0, 1, 2, 3]]
     t0 = wg[:, 1].min()
     span = (wg[:, 2] - wg[:, 1]) * 10
     start = (wg[:, 1] - t0) * 10
