@@ -359,6 +359,18 @@ hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStre
     return n == 2 ? launch_step_ppo_2(p, a, s) : hipErrorNotSupported;
 }
 
+bool step_records(int n)
+{
+    switch (n) {
+    case 2: return step_records_t<2>();
+    case 4: return step_records_t<4>();
+    case 6: return step_records_t<6>();
+    case 8: return step_records_t<8>();
+    case 10: return step_records_t<10>();
+    default: return false;
+    }
+}
+
 bool fused_rollout_n(int n)
 {
     switch (n) {

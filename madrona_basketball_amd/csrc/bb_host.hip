@@ -1014,6 +1014,7 @@ static int64_t ppo_step_fused_min_worlds()
 static int32_t ppo_path(const bb_sim *s, bool opponent, uint32_t flags)
 {
     if (s->cfg.exec_mode != BB_EXEC_CUDA) return BB_PPO_PATH_HOST;
+    if (s->n != 2) return -1;  // bb_rollout_policy: the reference's 2-agent game only
     const int64_t W = s->cfg.num_worlds;
     if (!(flags & BB_ROLLOUT_PER_STEP) && !opponent && bb::fused_rollout_n(s->n) && W <= ppo_fused_max_worlds())
         return BB_PPO_PATH_FUSED_ROLLOUT;
@@ -1111,7 +1112,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         uint64_t *ts = nullptr;
         const char *tr = std::getenv("MADRONA_BB_PPO_TRACE");  // diagnostics: per-step clocks of workgroup 0
         const int64_t groups = (W + 31) / 32;
-        const size_t TP = 16;  // PPO_TRACE_POINTS (bb_kernels.hip)
+        const size_t TP = 24;  // PPO_TRACE_POINTS (bb_kernels.hip)
         const size_t words = (size_t)n * TP + 2 * (size_t)groups;  // per-step clocks of workgroup 0, per-workgroup span
         if (tr && *tr && hipMalloc(&ts, words * 8) == hipSuccess) r.diag_ts = ts;
         hipError_t e = bb::launch_rollout_policy(s->n, s->p, r, st);
@@ -1140,9 +1141,21 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
     if (step_fused) {
         // policy pass 0 on the sim's rows, then per step k one k_step_ppo:
         // step k, then policy pass k + 1 (or the value pass after the last step)
+        // (diagnostics: MADRONA_BB_PPO_STEP_DIAG skip bits, MADRONA_BB_PPO_STEP_TRACE
+        // a file that receives every launch's per-wave phase clocks)
+        static const uint32_t diag = [] {
+            const char *e = std::getenv("MADRONA_BB_PPO_STEP_DIAG");
+            return (uint32_t)(e && *e ? std::atoi(e) : 0);
+        }();
+        const char *trace = std::getenv("MADRONA_BB_PPO_STEP_TRACE");
+        const int64_t waves = (W + 31) / 32;
+        uint64_t *ts = nullptr;
+        if (trace && *trace && hipMalloc(&ts, (size_t)n * waves * bb::PPS_TRACE_POINTS * 8) != hipSuccess) ts = nullptr;
         hipError_t e = bb::launch_policy(pass(0, false), st);
         for (int32_t k = 0; k < n && e == hipSuccess; k++) {
             bb::PpoStepArgs a{};
+            a.diag = diag;
+            a.diag_ts = ts ? ts + (size_t)k * waves * bb::PPS_TRACE_POINTS : nullptr;
             a.w = policy_weights(w);
             a.trainee = trainee; a.stochastic = stochastic ? 1 : 0; a.seed = seed;
             a.step = step0 + (uint32_t)(k + 1);
@@ -1161,6 +1174,18 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 a.value = out->next_value;
             }
             e = bb::launch_step_ppo(s->n, s->p, a, st);
+        }
+        if (ts) {
+            std::vector<uint64_t> h((size_t)n * waves * bb::PPS_TRACE_POINTS);
+            if (e == hipSuccess && hipMemcpyAsync(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess) {
+                FILE *f = std::fopen(trace, "wb");
+                if (f) {
+                    std::fwrite(h.data(), 8, h.size(), f);
+                    std::fclose(f);
+                }
+            }
+            (void)hipFree(ts);
         }
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy fused step launch");
     }
@@ -1186,28 +1211,58 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         a.mt = ppo_split_mt();  // k_policy<2>: 276 registers, a policy wave fits beside a step wave on one SIMD
         return a;
     };
-    const bool split = !fused && !step_fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds();
+    // the split needs at least 32 worlds (one policy tile) per part
+    const bool split = !fused && !step_fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds() &&
+                       W >= 32 * (int64_t)ppo_split_parts();
     // steps 0 .. n-2 write the trainee's rows into buffer.obs[k + 1] only (the
     // sim's copy of them is read by nobody before the last step rewrites
-    // every row); the next policy pass reads them there
-    const bool rec_only = out->obs != nullptr && ppo_rec_only();
+    // every row); the next policy pass reads them there.  Only the agent-lane
+    // step kernel records (bb::step_records); elsewhere the policy pass keeps
+    // the record and reads the sim's rows.
+    const bool step_rec = bb::step_records(s->n);
+    const bool rec_only = out->obs != nullptr && ppo_rec_only() && step_rec;
     const int parts = split ? ppo_split_parts() : 1;
     constexpr int MP = bb_sim::MAX_PARTS;
     hipStream_t pst[MP] = {st, st, st, st};
     if (split) {
         if (!s->aux[0]) {
-            for (hipStream_t &a : s->aux)
-                if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) return fail(BB_ERR_HIP, "hipStreamCreate");
-            for (hipEvent_t &e : s->aux_ev)
-                if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(BB_ERR_HIP, "hipEventCreate");
+            // all streams and events or none: created into locals, committed together
+            hipStream_t as[MP - 1] = {};
+            hipEvent_t ae[2 * MP] = {};
+            bool ok = true;
+            for (hipStream_t &a : as) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+            for (hipEvent_t &e : ae) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+            if (!ok) {
+                for (hipStream_t a : as)
+                    if (a) (void)hipStreamDestroy(a);
+                for (hipEvent_t e : ae)
+                    if (e) (void)hipEventDestroy(e);
+                return fail(BB_ERR_HIP, "bb_rollout_policy: creating the split's streams / events");
+            }
+            for (int i = 0; i < MP - 1; i++) s->aux[i] = as[i];
+            for (int i = 0; i < 2 * MP; i++) s->aux_ev[i] = ae[i];
         }
         // every part starts after everything before the call on the caller's stream
-        (void)hipEventRecord(s->aux_ev[0], st);
-        for (int h = 1; h < parts; h++) {
+        hipError_t e = hipEventRecord(s->aux_ev[0], st);
+        for (int h = 1; h < parts && e == hipSuccess; h++) {
             pst[h] = s->aux[h - 1];
-            (void)hipStreamWaitEvent(pst[h], s->aux_ev[0], 0);
+            e = hipStreamWaitEvent(pst[h], s->aux_ev[0], 0);
         }
+        if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy split start");
     }
+    // the caller's stream continues after every part's work -- also after an
+    // error, so that nothing still queued on a part's stream outlives the call
+    // unordered (the caller may free or reuse the buffers it writes)
+    const auto join = [&]() -> hipError_t {
+        hipError_t first = hipSuccess;
+        for (int h = 1; h < parts; h++) {
+            hipError_t e = hipEventRecord(s->aux_ev[MP + h], pst[h]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[MP + h], 0);
+            if (e != hipSuccess) e = hipStreamSynchronize(pst[h]);  // ordered the hard way
+            if (first == hipSuccess) first = e;
+        }
+        return first;
+    };
     bb::Params sp[MP];
     int64_t pw0[MP], pcnt[MP];
     for (int h = 0; h < parts; h++) {
@@ -1244,25 +1299,30 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             }
             if (e == hipSuccess) {
                 bb::Params p = sp[h];
-                if (out->obs && k + 1 < n) {
+                if (out->obs && k + 1 < n && step_rec) {
                     p.rec_obs = out->obs + (int64_t)(k + 1) * W * bb::POL_IN + pw0[h] * bb::POL_IN;
                     p.rec_agent = trainee;
                     p.rec_only = rec_only ? 1 : 0;
                 }
                 e = bb::launch_step(s->n, p, pst[h]);
             }
-            if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy launch");
+            if (e != hipSuccess) {
+                (void)join();
+                return hip_fail(e, "bb_rollout_policy launch");
+            }
         }
     }
     if (final_needed && split) {  // each part's value pass on its own stream, beside the others' last steps
         for (int h = 0; h < parts; h++) {
             hipError_t e = bb::launch_policy(part_pass(pass(n, true), pw0[h], pcnt[h], sp[h]), pst[h]);
-            if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy final pass");
+            if (e != hipSuccess) {
+                (void)join();
+                return hip_fail(e, "bb_rollout_policy final pass");
+            }
         }
     }
-    for (int h = 1; h < parts; h++) {  // the caller's stream continues after every part
-        hipError_t e = hipEventRecord(s->aux_ev[MP + h], pst[h]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(st, s->aux_ev[MP + h], 0);
+    {
+        const hipError_t e = join();
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy join");
     }
     if (final_needed && !fused && !split && !step_fused) {

@@ -929,25 +929,35 @@ __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, c
 //      into X (and on the last step every row into the sim's tensor);  -> barrier
 // then P's value pass over the final X gives next_value (ppo.py:136-137), and S
 // stores every column of the worlds (the state after step K-1).
-// Policy waves: two per 16-row M-tile, wave h of a pair running output columns
-// 16h..16h+15 of every product and the LayerNorm of half the rows
-// (policy_layers_half: PPO_LAYER_BARS workgroup barriers per pass, which the
-// sim wave passes while it waits), then the bucket pass of 8 rows.
+// Policy waves: one per 16-row M-tile (policy_layers1_split: both output
+// halves of every product in the one wave, the LayerNorms on its own
+// registers), so nothing inside the network crosses waves: a step has four
+// workgroup barriers -- X's first half ready, its second half, the actions,
+// X free.  (Until round 5 two waves per M-tile ran one output half each and
+// exchanged accumulators for the LayerNorms: five more barriers per step,
+// 8 192-world trace 4.56 us for the policy pass.)
 // The waves of the PPO workgroup share nothing through global memory inside
 // the loop, so their hand-offs are lds_barrier()s, which do not wait for the
 // wave's outstanding global stores (a __syncthreads() release fence does:
 // vmcnt(0) before every hand-off, ~1 us of write latency per step).
-constexpr int PPO_PWAVES = 4;
-constexpr int PPO_LAYER_BARS = 5;
+// BB_PPO_PWAVES=4 (A/B): two policy waves per M-tile, one output half each
+// (policy_layers_half_split), accumulators exchanged through LDS for the
+// LayerNorms: 5 more workgroup barriers per step, 8 rows per bucket pass.
+#ifndef BB_PPO_PWAVES
+#define BB_PPO_PWAVES 2
+#endif
+constexpr int PPO_PWAVES = BB_PPO_PWAVES;
+constexpr int PPO_LAYER_BARS = PPO_PWAVES == 4 ? 5 : 0;
+constexpr int PPO_ROWS = 32 / PPO_PWAVES;  // rows per policy wave's bucket pass
 constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
 struct PpoLds {
     float x[32][PPO_XS];
     int32_t act[32][6];
     float norm[2][POL_IN];
-    float ptile[2][16][33];   // hidden activations of each M-tile
-    float ltile[2][16][33];   // logits + value of each M-tile
-    HalfExchange ex[2];
-    BucketLds<8> bucket[PPO_PWAVES];
+    float ptile[2][16][33];   // each M-tile's hidden activations, then (2 waves) logits + value
+    float ltile[PPO_PWAVES == 4 ? 2 : 1][16][33];  // (4 waves) logits + value of each M-tile
+    HalfExchange ex[PPO_PWAVES == 4 ? 2 : 1];
+    BucketLds<PPO_ROWS> bucket[PPO_PWAVES];
     double erf[ERF_WORDS];
 };
 
@@ -972,12 +982,13 @@ struct LdsRowSink {
 };
 
 // diagnostics (PolicyRolloutArgs::diag_ts, workgroup 0): per step k the clock
-// at 0 S starts the step, 1 S's systems + reward done, 2 S's observation rows
-// done, 3 the first policy wave's actions done (for step k); the first policy
-// wave's pass for step k: 4 start (X holds the rows), 5 obs_out recorded, 6 X
-// in registers, 7-11 at the five barriers of the layers (after each), 12
-// bucket pass done.
-constexpr int PPO_TRACE_POINTS = 16;
+// at 0 S starts the step (the actions are in LDS), 1 S's systems done, 20 S's
+// row sources (intrinsic blocks) done, 21 S's half-rows of pass 0 in X, 2 the
+// rows complete, 3 the first policy wave's actions done (for step k); the
+// first policy wave's pass for step k: 4 start (pass 0 of X in LDS), 5 (the
+// same), 6 layer-1 steps 0..15 issued, 7 the rows' second half in LDS, 8-12
+// at the five barriers of the layers (after each), 13-16 bucket pass stamps.
+constexpr int PPO_TRACE_POINTS = 24;
 __device__ __forceinline__ void ppo_trace(const PolicyRolloutArgs &r, int t, int point)
 {
     if (r.diag_ts && blockIdx.x == 0) {
@@ -996,9 +1007,68 @@ __device__ __forceinline__ void ppo_trace_wg(const PolicyRolloutArgs &r, int whi
     }
 }
 
+// The trainee's observation row in two hand-offs: pass P holds row floats i
+// with ((i >> 4) & 1) == P (for every lane group q of layer 1 the chain steps
+// j = 16P .. 16P + 15), written at their own positions of X.  With ROLE >= 0
+// the world's two lanes share a pass: the trainee's lane (ROLE 0) writes the
+// floats with ((i >> 3) & 1) == 0, the other lane (ROLE 1, the trainee's row
+// emitted from its own view, observer slot 1) the rest.
+template <int P, int ROLE>
+struct XPassSink {
+    float *row;
+    float b0, b1, b2, b3;
+    int idx;
+    __device__ void put(float v)
+    {
+        if (((idx >> 4) & 1) == P && (ROLE < 0 || ((idx >> 3) & 1) == ROLE)) {
+            switch (idx & 3) {
+            case 0: b0 = v; break;
+            case 1: b1 = v; break;
+            case 2: b2 = v; break;
+            default: *(float4 *)(row + (idx & ~3)) = make_float4(b0, b1, b2, v); break;
+            }
+        }
+        idx++;
+    }
+    __device__ void put3(F3 v) { put(v.x); put(v.y); put(v.z); }
+    __device__ void put4(Q4 q) { put(q.w); put(q.x); put(q.y); put(q.z); }
+    __device__ void finish() { while (idx & 3) put(0.f); }
+};
+
+// Pass P of the trainee's row of the lane's world into X (row xr).  split:
+// both lanes of the world emit (shared intrinsic blocks, canonical slots);
+// otherwise the trainee's lane emits the pass alone (a non-canonical world's
+// whole row in pass 0, by the runtime-indexed sink).
+template <int P>
+__device__ __forceinline__ void ppo_x_pass(const World<2> &v, const Ctx &c, const SharedObs<2> &sh, bool active,
+                                           bool is_trainee, bool split, bool fast, float *xr, int32_t ib)
+{
+    if (!active) return;
+    if (split) {
+        if (is_trainee) {
+            XPassSink<P, 0> o;
+            o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+            emit_row_shared(v, c, sh, 0, o, ib);
+        } else {
+            XPassSink<P, 1> o;
+            o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+            emit_row_shared(v, c, sh, 1, o, ib);
+        }
+    } else if (is_trainee) {
+        if (fast) {
+            XPassSink<P, -1> o;
+            o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
+            emit_row_fast(v, c, 0, o, ib);
+        } else if (P == 0) {
+            fill_obs_slow(v, c, 0, xr, ib);
+        }
+    }
+}
+
 template <int N>
 __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, float *tile)
 {
+    static_assert(N == 2, "the reference's 2-agent game");
     ppo_trace_wg(r, 0);
     const int lane = threadIdx.x;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
@@ -1022,6 +1092,8 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
     }
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): no load pending into the loop
     lds_barrier();  // setup: X holds the trainee rows of step 0, the erf table is in LDS
+    lds_barrier();  // (step 0's two row hand-offs: X is complete already)
+    lds_barrier();
     for (int t = 0; t < r.steps; t++) {
         int lane_t = lane;
         int64_t w_t = w;
@@ -1054,26 +1126,29 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             agent_view(s, v, k);
         }
         ppo_trace(r, t, 1);
-        lds_barrier();  // X is free: the policy waves have recorded buffer.obs[t] from it
-        // the trainee's next observation row into X
-        {
-            SharedObs<N> sh;
-            lane_shared_obs(v, c, active, sh);
-            if (active && k == trainee) {
-                float *xr = L.x[wl];
-                if (share) {
-                    LdsRowSink o;
-                    o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
-                    emit_row_shared(v, c, sh, 0, o, ib);
-                } else if (canonical_slots(v, 0)) {
-                    LdsRowSink o;
-                    o.row = xr; o.idx = 0; o.b0 = o.b1 = o.b2 = o.b3 = 0.f;
-                    emit_row_fast(v, c, 0, o, ib);
-                } else {
-                    fill_obs_slow(v, c, 0, xr, ib);
-                }
-            }
+        // the trainee's next observation row into X, in two hand-offs
+        SharedObs<N> sh;
+        lane_shared_obs(v, c, active, sh);
+        const bool is_trainee = k == trainee;
+        const bool fast = active && canonical_slots(v, 0);
+        const bool split = share && fast;  // uniform over the world's two lanes
+        if (active && split && !is_trainee) {
+            // the trainee's direction / distance to this lane's agent, as the
+            // trainee's lane computes them (lane_shared_obs: to = other - self)
+            const F3 to = v.pos(0) - v.pos(1);
+            const float l2 = len2(to);
+            const float rr = 1.0f / bbm::sqrtf_(l2);
+            sh.rdir[1][0] = l2 > 1e-6f ? to * rr : f3(0.f, 0.f, 0.f);
+            sh.rlen[1][0] = bbm::sqrtf_(l2);
         }
+        ppo_trace(r, t, 20);
+        float *xr = L.x[wl];
+        lds_barrier();  // X is free: the policy waves have recorded buffer.obs[t] from it
+        ppo_x_pass<0>(v, c, sh, active, is_trainee, split, fast, xr, ib);
+        wave_sync();
+        ppo_trace(r, t, 21);
+        lds_barrier();  // pass 0 of X: the policy waves start layer 1
+        ppo_x_pass<1>(v, c, sh, active, is_trainee, split, fast, xr, ib);
         if (t + 1 == r.steps) {  // the sim's observation tensor: every row of the last step
             obs_pass_wave<N, 0>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
             wave_sync();
@@ -1105,12 +1180,14 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
 
 __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
 {
+    constexpr int RW = PPO_ROWS;                              // this wave's rows (bucket pass, records)
     const int lane = threadIdx.x % WAVE, c = lane & 15, q = lane >> 4;
     const int64_t W = p.num_worlds;
-    const int m = pw >> 1, h = pw & 1;                        // M-tile, column half
+    const int m = PPO_PWAVES == 4 ? pw >> 1 : pw;             // M-tile
+    const int h = PPO_PWAVES == 4 ? pw & 1 : 0;               // (4 waves) column half
     const int r0 = 16 * m;                                    // first X row of the M-tile
-    const int64_t row0 = (int64_t)blockIdx.x * 32 + r0;       // its first world
-    const int rh = 8 * h;                                     // this wave's 8 rows of the tile (bucket pass, records)
+    const int rh = RW * h;                                    // this wave's rows of the M-tile
+    const int64_t row0 = (int64_t)blockIdx.x * 32 + r0;       // the M-tile's first world
     // network constants: norm by the lanes of the policy waves, B operands per lane
     for (int k = pw * WAVE + lane; k < POL_IN; k += PPO_PWAVES * WAVE) {
         L.norm[0][k] = r.w.obs_mean[k];
@@ -1118,9 +1195,9 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     }
     PolicyRegs R;
     load_policy_regs(R, r.w, c, q);
-    // X for step 0: the trainee rows of the sim's observation tensor (with
-    // their zero tail, which emit never writes)
-    for (int i = lane; i < 8 * 32; i += WAVE) {
+    // X for step 0: this wave's trainee rows of the sim's observation tensor
+    // (with their zero tail, which emit never writes)
+    for (int i = lane; i < RW * 32; i += WAVE) {
         const int rr = r0 + rh + i / 32, qq = i % 32;
         const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
         float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1133,48 +1210,49 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     a.rows = W;
     a.stochastic = r.stochastic;
     a.seed = r.seed;
-    auto bar = [] { lds_barrier(); };
     // the sampling uniforms of a step depend on (seed, step, row, bucket) only: each
     // step's is drawn while the sim wave runs the step before it
-    BucketNoise<8> noise;
-    if (r.stochastic) bucket_noise<8>(noise, r.seed, r.step0, row0 + rh, W, lane);
+    BucketNoise<RW> noise;
+    if (r.stochastic) bucket_noise<RW>(noise, r.seed, r.step0, row0 + rh, W, lane);
     for (int t = 0; t <= r.steps; t++) {
         const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
         const bool tr = pw == 0 && !final_pass;
+        lds_barrier();  // pass 0 of X: the rows' first half
         if (tr) ppo_trace(r, t, 4);
         if (tr) ppo_trace(r, t, 5);
-        float x[32];
-#pragma unroll
-        for (int v = 0; v < 8; v++) {
-            const float4 o = *(const float4 *)&L.x[r0 + c][32 * q + 4 * v];
-            x[4 * v] = o.x; x[4 * v + 1] = o.y; x[4 * v + 2] = o.z; x[4 * v + 3] = o.w;
-        }
-        if (r.diag_ts) {  // (diagnostics: the loads retired here, and a clock at every barrier)
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+        auto mid = [&] {
             if (tr) ppo_trace(r, t, 6);
-            int nb = 0;
-            auto tbar = [&] { if (tr) ppo_trace(r, t, 7 + nb); nb++; lds_barrier(); };
-            policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, tbar);
+            lds_barrier();  // the rows' second half
+            if (tr) ppo_trace(r, t, 7);
+        };
+        float (*lt)[33];
+        if constexpr (PPO_PWAVES == 4) {
+            auto bar = [] { lds_barrier(); };
+            policy_layers_half_split(&L.x[r0 + c][0], R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, mid,
+                                     bar);
+            lt = L.ltile[m];
         } else {
-            policy_layers_half(x, R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, bar);
+            policy_layers1_split(&L.x[r0 + c][0], R, L.norm, L.ptile[m], c, q, mid);
+            lt = L.ptile[m];
         }
+        if (tr) ppo_trace(r, t, 12);
         a.step = r.step0 + (uint32_t)t;
         if (!final_pass) {
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
-            uint64_t *bts = (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 12 : nullptr;
+            uint64_t *bts = (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 13 : nullptr;
             if (r.stochastic)
-                bucket_pass_spread<8, true>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise, bts);
+                bucket_pass_spread<RW, true>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise, bts);
             else
-                bucket_pass_spread<8, false>(a, L.ltile[m] + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr, bts);
+                bucket_pass_spread<RW, false>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr, bts);
             pol_wave_sync();
             if (pw == 0) ppo_trace(r, t, 3);
             lds_barrier();  // actions in LDS
-            // while the sim wave steps: buffer.obs[t] = X (this wave's 8 rows),
+            // while the sim wave steps: buffer.obs[t] = X (this wave's rows),
             // then the next step's sampling uniforms
             if (r.obs_out) {
-                for (int i = lane; i < 8 * 32; i += WAVE) {
+                for (int i = lane; i < RW * 32; i += WAVE) {
                     const int rr = r0 + rh + i / 32, qq = i % 32;
                     const int64_t wg = (int64_t)blockIdx.x * 32 + rr;
                     if (wg < W)
@@ -1182,17 +1260,19 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
                 }
             }
             if (r.stochastic && t + 1 < r.steps)
-                bucket_noise<8>(noise, r.seed, r.step0 + (uint32_t)(t + 1), row0 + rh, W, lane);
+                bucket_noise<RW>(noise, r.seed, r.step0 + (uint32_t)(t + 1), row0 + rh, W, lane);
             lds_barrier();  // X is free (the sim wave rewrites it next)
-            lds_barrier();  // X holds the observations after step t
-        } else if (r.next_value && lane < 8 && row0 + rh + lane < W) {
-            r.next_value[row0 + rh + lane] = L.ltile[m][rh + lane][POL_LOGITS];
+        } else if (r.next_value && lane < RW && row0 + rh + lane < W) {
+            r.next_value[row0 + rh + lane] = lt[rh + lane][POL_LOGITS];
         }
     }
 }
 
-template <int N>
-__global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), 1) void k_rollout_policy(const Params p, const PolicyRolloutArgs r)
+// MINW: waves per SIMD the register budget is sized for -- 1 while the grid
+// is one workgroup per CU (each of its 3 waves then has a SIMD to itself and
+// the sim wave keeps its world without spills), 2 above
+template <int N, int MINW>
+__global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), MINW) void k_rollout_policy(const Params p, const PolicyRolloutArgs r)
 {
     if constexpr (N == 2 && FusedRollout<N>::value) {
         __shared__ PpoLds L;
@@ -1224,6 +1304,11 @@ __global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), 1) void k_rollout_policy(c
 // (PolicyLdsWeights, 32.6 KB); each wave's tile (64 rows x 60 floats, 15 KB)
 // takes the LayerNorm / bucket-pass exchanges after the last pass.
 constexpr int PPS_RS = 60;  // tile row stride (floats): 14 pieces + 1, == 4 mod 8 dwords
+// buffer.obs rows (half lines per pass): write-through -- measured at 65 536
+// worlds 39.3 us per step vs 40.5 nt, 42.3 plain (profiles/r05/c_rec_policy_ab.txt)
+#ifndef BB_PPS_REC_AUX
+#define BB_PPS_REC_AUX 16
+#endif
 constexpr int PPS_TILE = WAVE * PPS_RS;
 
 template <int WPG>
@@ -1351,7 +1436,7 @@ __device__ __forceinline__ void ppo_flush_pass(const float *tile, char *obs, cha
         }
 #pragma unroll
         for (int i = 0; i < RIT; i++)
-            if (ok[i]) row_store<BB_REC_AUX>(rec, off[i], v[i]);
+            if (ok[i]) row_store<BB_PPS_REC_AUX>(rec, off[i], v[i]);
     }
 }
 
@@ -1372,6 +1457,19 @@ __device__ __forceinline__ void ppo_emit_pass(const World<2> &v, const Ctx &c, c
     }
 }
 
+// diagnostics (PpoStepArgs::diag_ts): the wave's clock at 0 start, 1 state
+// loaded, 2 systems done, 3 state stores issued, 4 pass 0 in the tile, 5 pass 0
+// MFMAs and stores issued, 6 pass 1 in the tile, 7 pass 1 issued, 8 layers
+// done, 9 bucket pass done, 10 the wave's stores retired
+__device__ __forceinline__ void pps_trace(const PpoStepArgs &a, int64_t gw, int point, bool wait_mem = false)
+{
+    if (a.diag_ts) {
+        if (wait_mem) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint64_t t = wall_clock64();
+        if ((threadIdx.x & 63) == 0) a.diag_ts[gw * PPS_TRACE_POINTS + point] = t;
+    }
+}
+
 template <int WPG, bool LAST>
 __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs &a, PpoStepLds<WPG> &S, int wave,
                                               int lane)
@@ -1385,9 +1483,21 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     const int trainee = a.trainee;
     const LaneAgents<N, MODE_FULL> ag{k, &p};
 
+    const int64_t gw = (int64_t)blockIdx.x * WPG + wave;
     World<N> s;
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;
+    pps_trace(a, gw, 0);
+    // (timing experiment, PpoStepArgs::diag bits 8-15: the upper half of the
+    // workgroup's waves -- one of the two waves of each SIMD -- starts that
+    // many s_sleep(127) later, the weights copied and published first)
+    const uint32_t skew = (a.diag >> 8) & 0xFFu;
+    if (skew) {
+        policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
+        lds_barrier();
+        if (wave >= WPG / 2)
+            for (uint32_t i = 0; i < skew; i++) __builtin_amdgcn_s_sleep(127);
+    }
     if (active) {
         load_world(s, p, w);
         {
@@ -1399,9 +1509,16 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
             park_words(tile, lane, x);
         }
     }
+    // the policy's sampling uniforms for step k + 1 (they depend on the seed,
+    // step, row and bucket only): drawn while the state loads are in flight,
+    // off the bucket pass's chain
+    BucketNoise<32> noise;
+    if (!LAST && a.stochastic) bucket_noise<32>(noise, a.seed, a.step, w0, p.num_worlds, lane);
+    pps_trace(a, gw, 1, true);
     // the workgroup's copy of the network (read after the barrier below)
-    policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
+    if (!skew) policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
     if (active) step_world_pre_obs(s, c, ag);
+    pps_trace(a, gw, 2);
     if (active) {
         agent_view(s, v, k);
         sys_reward_agent(v, 0, AGENT0_ID + k);
@@ -1417,40 +1534,54 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
             a.done[w] = v.done[0];
         }
     }
+    pps_trace(a, gw, 3);
     const int32_t ib = active ? inbounder_id(s) : -1;
     const bool share = active && obs_sharable(s);
     SharedObs<N> sh;
     lane_shared_obs(v, c, active, sh);
     const bool fast = active && canonical_slots(v, 0);
     const uint64_t live = __ballot(active);
+    const uint32_t diag = a.diag;  // (0 outside timing diagnostics)
     char *obs = (char *)(p.c.obs + w0 * N * (int64_t)obs_width(N));                // wave-uniform
-    char *rec = (!LAST && a.obs_rec) ? (char *)(a.obs_rec + w0 * (int64_t)POL_IN) : nullptr;
+    char *rec = (!LAST && a.obs_rec && !(diag & 8u)) ? (char *)(a.obs_rec + w0 * (int64_t)POL_IN) : nullptr;
     const int pl = lane & 15, pq = lane >> 4;
     f32x4 acc[2][2];
 #pragma unroll
     for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     wave_sync();  // the parked words are read
     ppo_emit_pass<0>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
-    lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
-    ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
+    if (!skew) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
+    else wave_sync();
+    pps_trace(a, gw, 4);
+    if (!(diag & 4u)) ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
     ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
+    pps_trace(a, gw, 5);
     ppo_emit_pass<1>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
     wave_sync();
-    ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
+    pps_trace(a, gw, 6);
+    if (!(diag & 4u)) ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
     ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
+    pps_trace(a, gw, 7);
     if (LAST && !a.value) return;  // (wave-uniform; no barrier follows)
     // LayerNorm 1, layer 2, heads (the tile's first 32 x 33 floats), then the
     // bucket pass (its exchange right behind them)
     float (*lt)[33] = (float (*)[33])tile;
+    if (!(diag & 2u)) {
 #pragma unroll
-    for (int mt = 0; mt < 2; mt++)
-        ln_relu_to_tile(acc[mt][0], acc[mt][1], S.wt.cst[0][pl], S.wt.cst[0][pl + 16], S.wt.cst[1][pl],
-                        S.wt.cst[1][pl + 16], S.wt.cst[2][pl], S.wt.cst[2][pl + 16], lt + 16 * mt, pl, pq);
-    pol_wave_sync();
-#pragma unroll
-    for (int mt = 0; mt < 2; mt++) policy_tail_lds(S.wt, lt + 16 * mt, pl, pq);
+        for (int mt = 0; mt < 2; mt++)
+            ln_relu_to_tile(acc[mt][0], acc[mt][1], S.wt.cst[0][pl], S.wt.cst[0][pl + 16], S.wt.cst[1][pl],
+                            S.wt.cst[1][pl + 16], S.wt.cst[2][pl], S.wt.cst[2][pl + 16], lt + 16 * mt, pl, pq);
+        pol_wave_sync();
+        policy_tail_lds2(S.wt, lt, pl, pq);
+    }
+    pps_trace(a, gw, 8);
+    if (diag & 1u) {
+        pps_trace(a, gw, 9);
+        pps_trace(a, gw, 10, true);
+        return;
+    }
     if constexpr (LAST) {
         if (a.value && lane < 32 && w0 + lane < p.num_worlds) a.value[w0 + lane] = lt[lane][POL_LOGITS];
     } else {
@@ -1465,8 +1596,11 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
         pa.log_prob = a.log_prob;
         pa.value = a.value;
         BucketLds<32> &bl = *(BucketLds<32> *)(tile + 32 * 33);
-        bucket_pass_spread<32>(pa, lt, w0, lane, bl);
+        if (a.stochastic) bucket_pass_spread<32, true, 1>(pa, lt, w0, lane, bl, nullptr, &noise);
+        else bucket_pass_spread<32, true, 0>(pa, lt, w0, lane, bl, nullptr, &noise);
     }
+    pps_trace(a, gw, 9);
+    pps_trace(a, gw, 10, true);
 }
 
 template <int WPG, bool LAST>
@@ -1742,8 +1876,8 @@ __device__ __forceinline__ void read_batch(const float *e, const int (&src)[NP][
                           e[src[p][A0 + b][2] + (dtm[p][2] & tm)], e[src[p][A0 + b][3] + (dtm[p][3] & tm)]};
     }
 }
-template <int N, int AUX, int S0, int S1, int NP, int RB, int A0>
-__device__ __forceinline__ void emit_slot_batches(const SharedLds<N> &sm, const int (&src)[NP][N][4],
+template <int N, int AUX, int S0, int S1, int NP, int RB, int A0, class SM>
+__device__ __forceinline__ void emit_slot_batches(const SM &sm, const int (&src)[NP][N][4],
                                                   const int (&dtm)[NP][4], uint64_t rows, uint64_t teams, char *base,
                                                   int lane, int slot, vf4 (&cur)[RB][NP])
 {
@@ -1766,14 +1900,14 @@ __device__ __forceinline__ void emit_slot_batches(const SharedLds<N> &sm, const 
     for (int b = 0; b < RB; b++)
 #pragma unroll
         for (int p = 0; p < NP; p++) cur[b][p] = nxt[b][p];
-    if constexpr (A0 + RB < N) emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB>(sm, src, dtm, rows, teams, base, lane, slot, cur);
+    if constexpr (A0 + RB < N) emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB, SM>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
-template <int N, int AUX, int S0, int S1>
-__device__ __forceinline__ void emit_pieces_rows(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+template <int N, int AUX, int S0, int S1, class SM>
+__device__ __forceinline__ void emit_pieces_rows(const SM &sm, uint64_t rows, uint64_t teams, float *obs,
                                                  int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
-    constexpr int WPW = SharedLds<N>::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
+    constexpr int WPW = SM::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
     constexpr int RB = (BB_OBS_RB > 0 && N % (BB_OBS_RB > 0 ? BB_OBS_RB : 1) == 0) ? BB_OBS_RB : (NP == 1 ? N : 2);
     static_assert(N % RB == 0, "whole read batches per slot");
     int src[NP][N][4], dtm[NP][4];
@@ -1790,34 +1924,34 @@ __device__ __forceinline__ void emit_pieces_rows(const SharedLds<N> &sm, uint64_
         }
     }
     char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
-    static_assert(S1 <= WPW && S1 - S0 <= SharedLds<N>::SPP, "part of the source table");
+    static_assert(S1 <= WPW && S1 - S0 <= SM::SPP, "part of the source table");
     vf4 cur[RB][NP];
     read_batch<N, NP, RB, 0>(sm.e[0], src, dtm, teams >> (S0 * N), cur);
     for (int slot = S0; slot < S1; slot++)
-        emit_slot_batches<N, AUX, S0, S1, NP, RB, 0>(sm, src, dtm, rows, teams, base, lane, slot, cur);
+        emit_slot_batches<N, AUX, S0, S1, NP, RB, 0, SM>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
 
-template <int N, int AUX, int S0 = 0, int S1 = SharedLds<N>::WPW>
-__device__ __forceinline__ void emit_pieces(const SharedLds<N> &sm, uint64_t rows, uint64_t teams, float *obs,
+template <int N, int AUX, int S0, int S1, class SM>
+__device__ __forceinline__ void emit_pieces(const SM &sm, uint64_t rows, uint64_t teams, float *obs,
                                             int64_t row0, int lane)
 {
-    emit_pieces_rows<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
+    emit_pieces_rows<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane);
 }
 
 // The source table written and emitted part by part (BB_OBS_PARTS): the
 // world state is dead once every lane holds its sources; each part's lanes
 // put theirs, the wave emits that part's rows, and the next part overlays it.
-template <int N, int AUX, int P = 0>
-__device__ __forceinline__ void obs_parts(SharedLds<N> &sm, const LaneSources<N> &src, uint64_t rows, uint64_t teams, float *obs,
+template <int N, int AUX, int P = 0, class SM = SharedLds<N>>
+__device__ __forceinline__ void obs_parts(SM &sm, const LaneSources<N> &src, uint64_t rows, uint64_t teams, float *obs,
                                           int64_t row0, int lane, int slot, int k, bool active, bool share)
 {
-    using SL = SharedLds<N>;
+    using SL = SM;
     constexpr int S0 = P * SL::SPP, S1 = (S0 + SL::SPP < SL::WPW) ? S0 + SL::SPP : SL::WPW;
     __syncthreads();  // the world state (or the previous part) is dead: this part overlays it
     if (active && slot >= S0 && slot < S1) src.put(sm.e[slot - S0], k, share);
     __syncthreads();
-    emit_pieces<N, AUX, S0, S1>(sm, rows, teams, obs, row0, lane);
-    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1>(sm, src, rows, teams, obs, row0, lane, slot, k, active, share);
+    emit_pieces<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane);
+    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1, SM>(sm, src, rows, teams, obs, row0, lane, slot, k, active, share);
 }
 
 template <int N, int MODE, int PHASE = 0>
@@ -1991,6 +2125,163 @@ __device__ __forceinline__ void step_shared_world(const Params &p, float *tile, 
     }
 }
 
+// K steps per launch with the world in LDS (bb_rollout at N >= 4, SURVEY
+// 8(f) rank 4; scripts/ppo.py:65): step_shared_world's step K times over the
+// world the wave loaded once.  Per step only the action rows come in
+// (actions[t], the defence AI's overrides written back there, as the per-step
+// launches leave them) and the observation rows, rewards and done flags go
+// out (obs/reward/done + t * step); the state columns are stored once, after
+// the last step.  The row-source table of the observation pass overlays the
+// world state (SharedLds), so each lane keeps 1/N of the world's words in
+// registers across the pass and writes them back after it.
+// At N >= 6 the register copy (45+ words per lane on top of the row pass's
+// row sources and decode tables) spills: there the source table sits beside
+// the world instead (SharedLdsRoll: more LDS per wave, fewer waves per CU).
+template <int N>
+struct SharedLdsRoll {
+    static constexpr int WPW = WAVE / N, PARTS = 1, SPP = WPW;
+    World<N> world[WPW];
+    uint32_t x[DppAgents<N>::value ? 1 : WAVE][XW];
+    float e[SPP][ObsSrc<N>::ES];
+    uint4 code[obs_width(N) / 4];
+};
+template <int N>
+struct SharedRollout {
+    static constexpr bool value = Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value;
+    static constexpr bool KEEP = N == 4;  // the world's words in registers across the row pass (else SharedLdsRoll)
+    static constexpr int WORDS = (int)(sizeof(World<N>) / 4);
+    static constexpr int CH = KEEP ? (WORDS + N - 1) / N : 1;  // words a lane keeps across the row pass
+    using Lds = typename std::conditional<KEEP, SharedLds<N>, SharedLdsRoll<N>>::type;
+};
+
+template <int N, class SM>
+__device__ __forceinline__ void rollout_shared_world(const Params &p, const RolloutArgs &r, SM &sm)
+{
+    using SR = SharedRollout<N>;
+    constexpr int WPW = SM::WPW, OW = obs_width(N);
+    constexpr int AUX = BB_ROLLOUT_AUX;  // rows into a fresh [K][W][N][OBSW] buffer
+    const int lane = threadIdx.x;
+    const bool lane_used = lane < WPW * N;
+    const int slot = lane_used ? lane / N : WPW - 1;
+    const int k = lane_used ? lane % N : (lane - WPW * N) % N;
+    const int64_t w0 = (int64_t)blockIdx.x * WPW;
+    const int64_t w = w0 + slot;
+    const int64_t W = p.num_worlds;
+    const bool world_ok = w < W;
+    const bool active = lane_used && world_ok;
+    World<N> &s = sm.world[slot];
+    using AG = typename std::conditional<DppAgents<N>::value, LaneAgents<N, MODE_FULL, true>, LdsAgents<N, MODE_FULL>>::type;
+    AG ag;
+    if constexpr (DppAgents<N>::value) ag = LaneAgents<N, MODE_FULL, true>{k, &p};
+    else ag = LdsAgents<N, MODE_FULL>{k, slot, sm.x, &p};
+    if (active) {
+        AgentRaw<N> ar;
+        WorldRaw wr;
+        ar.load(p, w, k);
+        if (k == 0) wr.load(p, w);
+        ar.commit(s, k);
+        if (k == 0) wr.commit(s);
+    }
+    for (int t = 0; t < r.steps; t++) {
+        // per-step opaque copies of the lane's indices: what derives from them
+        // (the row pass's decode tables, column addresses) is recomputed in
+        // the iteration instead of being hoisted out of the loop and held in
+        // registers across every step (k_rollout's discipline)
+        int lane_t = lane, k_t = k;
+        int64_t w_t = w;
+        __asm__ volatile("" : "+v"(lane_t));
+        __asm__ volatile("" : "+v"(k_t));
+        __asm__ volatile("" : "+v"(w_t));
+        const int64_t row = w_t * N + k_t;  // the lane's agent row
+        Ctx c = make_ctx(p, w_t, active && k_t == 0);
+        // the action row of step t (actions[t] stands in for the action column)
+        int32_t *acts = r.actions + (int64_t)t * W * N * 6;
+        if (active) {
+            uint32_t a6[6];
+            load_words<6>(acts, row, a6);
+#pragma unroll
+            for (int q = 0; q < 6; q++) s.act[k_t][q] = (int32_t)a6[q];
+        }
+        __syncthreads();
+        step_world_pre_obs(s, c, ag);
+        __syncthreads();
+        const float rw = reward_one(s, k_t, AGENT0_ID + k_t);
+        __syncthreads();  // every lane has read the rewards it needs
+        if (lane_used) s.rew[k_t] = rw;
+        __syncthreads();
+        if (active) {
+            uint32_t a6[6];
+#pragma unroll
+            for (int q = 0; q < 6; q++) a6[q] = (uint32_t)s.act[k_t][q];
+            store_words<6>(acts, row, a6);  // with the defence AI's overrides
+            r.reward[(int64_t)t * r.rd_step + row] = s.rew[k_t];
+            r.done[(int64_t)t * r.rd_step + row] = s.done[k_t];
+        }
+        // observation rows of step t
+        float *obs_t = r.obs + (int64_t)t * r.obs_step;
+        const int32_t ib = inbounder_id(s);
+        const bool share = obs_sharable(s);
+        LaneSources<N> src;
+        if (active) {
+            src.compute(s, c, k_t, ib, share);
+            if (!share) {  // rows the pieces do not cover: straight from the lane
+                float *grow = obs_t + row * (int64_t)OW;
+                if (canonical_slots(s, k_t)) fill_obs_fast(s, c, k_t, grow, ib);
+                else fill_obs_slow(s, c, k_t, grow, ib);
+            }
+        }
+        const uint64_t rows = __ballot(active && share);
+        const uint64_t teams = __ballot(active && share && src.tm != 0);
+        // the lane's share of the world's words, kept across the row pass
+        // (whose source table overlays the world)
+        uint32_t keep[SR::CH];
+        if constexpr (SR::KEEP) {
+            const uint32_t *ws = (const uint32_t *)&s;
+#pragma unroll
+            for (int i = 0; i < SR::CH; i++) {
+                const int idx = k_t * SR::CH + i;
+                keep[i] = idx < SR::WORDS ? ws[idx] : 0u;
+            }
+        }
+        obs_parts<N, AUX, 0, SM>(sm, src, rows, teams, obs_t, w0 * N, lane_t, slot, k_t, active, share);
+        __syncthreads();  // the table's readers are done
+        if constexpr (SR::KEEP) {
+            if (lane_used) {
+                uint32_t *ws = (uint32_t *)&s;
+#pragma unroll
+                for (int i = 0; i < SR::CH; i++) {
+                    const int idx = k_t * SR::CH + i;
+                    if (idx < SR::WORDS) ws[idx] = keep[i];
+                }
+            }
+            __syncthreads();
+        }
+    }
+    // the state after the last step, every column (the per-step launches'
+    // last stores; actions / rewards / done flags as the last step left them)
+    if (active) {
+        // (opaque copies: the column addresses are not shared with the loads
+        // before the loop and held across it)
+        int k_e = k;
+        int64_t w_e = w;
+        __asm__ volatile("" : "+v"(k_e));
+        __asm__ volatile("" : "+v"(w_e));
+        store_world_agent<N>(s, p, w_e * N + k_e, k_e);
+        if (k_e == 0) store_world_shared<N>(s, p, w_e);
+    }
+}
+
+template <int N>
+__global__ __launch_bounds__(WAVE, 2) void k_rollout_shared(const Params p, const RolloutArgs r)
+{
+    if constexpr (SharedRollout<N>::value) {
+        __shared__ typename SharedRollout<N>::Lds sm;
+        const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
+        for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
+        rollout_shared_world<N>(p, r, sm);
+    }
+}
+
 // One lane per world.
 template <int N, int MODE>
 __device__ __forceinline__ void step_world_lanes(const Params &p, float *tile)
@@ -2151,7 +2442,10 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
     constexpr int WPB = Lanes<N>::WPB;
     const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
 #define BB_LAUNCH(m) hipExtLaunchKernelGGL(k_step<N, m>, grid, block, 0, s, ev0, ev1, 0, p)
-    if constexpr (Lanes<N>::LPW == N && !Lanes<N>::SHARED) {
+    if (p.rec_obs && !(N == 2 && Lanes<N>::LPW == N && !Lanes<N>::SHARED))
+        return hipErrorNotSupported;  // a record the step cannot write (step_records_t)
+    if constexpr (N == 2 && Lanes<N>::LPW == N && !Lanes<N>::SHARED) {
+        static_assert(obs_width(N) == POL_IN, "the record rows are the sim's rows");
         if (mode == MODE_FULL && p.rec_obs) {
             if (step_lines<N>(p.num_worlds)) hipExtLaunchKernelGGL((k_step<N, MODE_FULL, true, true>), grid, block, 0, s, ev0, ev1, 0, p);
             else hipExtLaunchKernelGGL((k_step<N, MODE_FULL, false, true>), grid, block, 0, s, ev0, ev1, 0, p);
@@ -2205,7 +2499,12 @@ static bool rollout_split(unsigned groups)
 template <int N>
 hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
-    if constexpr (!FusedRollout<N>::value) {
+    if constexpr (SharedRollout<N>::value) {
+        constexpr int WPB = Lanes<N>::WPB;
+        const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+        hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        return hipGetLastError();
+    } else if constexpr (!FusedRollout<N>::value) {
         return hipErrorNotSupported;
     } else {
         constexpr int WPB = Lanes<N>::WPB;
@@ -2227,7 +2526,10 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
         return hipErrorNotSupported;
     } else {
         const dim3 grid((unsigned)((p.num_worlds + 31) / 32)), block(WAVE * (1 + PPO_PWAVES));
-        hipLaunchKernelGGL(k_rollout_policy<N>, grid, block, 0, s, p, r);
+        // (3 waves: each its own SIMD; 5 waves share them -- the 256-register budget)
+        if (PPO_PWAVES == 2 && grid.x <= device_cus())
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 1>), grid, block, 0, s, p, r);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2>), grid, block, 0, s, p, r);
         return hipGetLastError();
     }
 }
@@ -2264,7 +2566,8 @@ template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEve
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRolloutArgs &, hipStream_t);
-template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value; }
+template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value || SharedRollout<BB_N>::value; }
+template <> bool step_records_t<BB_N>() { return BB_N == 2 && Lanes<BB_N>::LPW == BB_N && !Lanes<BB_N>::SHARED; }
 template <> int step_grid<BB_N>(int64_t num_worlds)
 {
     return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB);  // waves of the MODE_FULL launch

@@ -61,7 +61,14 @@ struct PpoStepArgs {
     int32_t trainee, stochastic;
     int32_t last;               // the rollout's last step: every row into the sim's obs, value only
     uint32_t seed, step;        // the policy's sampling key (seed, step0 + k + 1)
+    // diagnostics only (timing attribution; the outputs are then wrong):
+    // diag bit 0 no bucket pass, 1 no LayerNorm-1 / layer 2 / heads, 2 no
+    // layer-1 MFMAs, 3 no buffer.obs stores; diag_ts: PPS_TRACE_POINTS clocks
+    // per wave
+    uint32_t diag;
+    uint64_t *diag_ts;
 };
+constexpr int PPS_TRACE_POINTS = 12;
 // N = 2 only (hipErrorNotSupported otherwise)
 hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s);
 
@@ -85,6 +92,7 @@ template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= wav
 template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
                                              hipEvent_t ev1);
 template <int N> bool fused_rollout();  // k_rollout<N> exists (else: one k_step launch per step)
+template <int N> bool step_records_t();  // k_step<N> honours Params::rec_obs
 template <int N> hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, hipStream_t s);
 
 #define BB_EXTERN_N(n)                                                                  \
@@ -93,6 +101,7 @@ template <int N> hipError_t launch_rollout_policy_t(const Params &p, const Polic
     template <> int step_grid<n>(int64_t);                                              \
     extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
     template <> bool fused_rollout<n>();                                                \
+    template <> bool step_records_t<n>();                                               \
     extern template hipError_t launch_rollout_policy_t<n>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 BB_EXTERN_N(2)
 BB_EXTERN_N(4)
@@ -107,6 +116,9 @@ hipError_t launch_init(int n, const Params &p, hipStream_t s);
 hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
                           hipEvent_t ev1 = nullptr);
 bool fused_rollout_n(int n);
+// whether k_step honours Params::rec_obs (PPO's buffer.obs record from the
+// step's row passes): the agent-lane kernel of the 2-agent game only
+bool step_records(int n);
 // fused PPO rollout (N = 2 only; hipErrorNotSupported otherwise)
 hipError_t launch_rollout_policy(int n, const Params &p, const PolicyRolloutArgs &r, hipStream_t s);
 int step_grid_n(int n, int64_t num_worlds);

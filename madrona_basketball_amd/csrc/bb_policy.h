@@ -64,23 +64,27 @@ constexpr int POL_TRACE_POINTS = 8;
 // exp / log in f32 from a fixed sequence of f32 operations (identical bits on
 // host and gfx950; ~1 ulp): the policy is compared with torch's fp32 forward
 // within a tolerance, so the step's correctly-rounded double route (bb_math)
-// is not needed here, and these are 4-8x cheaper.
+// is not needed here, and these are 4-8x cheaper.  The polynomials run as
+// explicit fused multiply-adds (correctly rounded on both sides: v_fma_f32 /
+// the host's fmaf), half the instructions of the separately rounded mul + add
+// chains (the translation units build with -ffp-contract=off) -- the bucket
+// pass evaluates 19 of these per row (round 5).
 BB_HD float pol_expf(float x)
 {
     if (x != x) return x;
     if (x > 88.7f) return __builtin_inff();
     if (x < -103.9f) return 0.f;
     const float k = __builtin_rintf(x * 1.44269504f);
-    float r = x - k * 0.693145752f;          // ln2 high part (exact product for |k| < 2^11)
-    r = r - k * 1.42860677e-06f;             // ln2 low part
-    float p = 1.0f / 5040.0f;                // Taylor to r^7 on |r| <= 0.347
-    p = p * r + 1.0f / 720.0f;
-    p = p * r + 1.0f / 120.0f;
-    p = p * r + 1.0f / 24.0f;
-    p = p * r + 1.0f / 6.0f;
-    p = p * r + 0.5f;
-    p = p * r + 1.0f;
-    p = p * r + 1.0f;
+    float r = __builtin_fmaf(-k, 0.693145752f, x);    // ln2 high part
+    r = __builtin_fmaf(-k, 1.42860677e-06f, r);        // ln2 low part
+    float p = 1.0f / 5040.0f;                          // Taylor to r^7 on |r| <= 0.347
+    p = __builtin_fmaf(p, r, 1.0f / 720.0f);
+    p = __builtin_fmaf(p, r, 1.0f / 120.0f);
+    p = __builtin_fmaf(p, r, 1.0f / 24.0f);
+    p = __builtin_fmaf(p, r, 1.0f / 6.0f);
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
     return __builtin_ldexpf(p, (int)k);
 }
 BB_HD float pol_logf(float x)
@@ -94,13 +98,13 @@ BB_HD float pol_logf(float x)
     const float s = (m - 1.0f) / (m + 1.0f);  // |s| <= 0.1716
     const float z = s * s;
     float p = 1.0f / 11.0f;
-    p = p * z + 1.0f / 9.0f;
-    p = p * z + 1.0f / 7.0f;
-    p = p * z + 1.0f / 5.0f;
-    p = p * z + 1.0f / 3.0f;
-    const float lm = 2.0f * (s + (s * z) * p);
+    p = __builtin_fmaf(p, z, 1.0f / 9.0f);
+    p = __builtin_fmaf(p, z, 1.0f / 7.0f);
+    p = __builtin_fmaf(p, z, 1.0f / 5.0f);
+    p = __builtin_fmaf(p, z, 1.0f / 3.0f);
+    const float lm = 2.0f * __builtin_fmaf(s * z, p, s);
     const float k = (float)e;
-    return k * 0.693145752f + (k * 1.42860677e-06f + lm);
+    return __builtin_fmaf(k, 0.693145752f, __builtin_fmaf(k, 1.42860677e-06f, lm));
 }
 BB_HD float pol_clamp(float x) { return __builtin_fminf(__builtin_fmaxf(x, -5.f), 5.f); }  // v_max / v_min
 BB_HD float pol_relu(float x) { return x > 0.f ? x : 0.f; }

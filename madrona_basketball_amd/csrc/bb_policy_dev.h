@@ -119,18 +119,19 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
 
 // Bucket pass of R < 64 rows: LPR = 64 / R lanes per row,
 // every step the same instructions on different data (no divergent roles):
-//   A  lane part p: e = exp(logit - bucket max) of logits p, p + LPR, ...,
-//      into LDS;
-//   B  lane part p: buckets p, p + LPR, ...: the action (first maximum, or
-//      the inverse-CDF draw over the bucket's e in logit order), sum of e in
-//      logit order, logit - logsumexp, into LDS;
+//   B  lane part p: buckets p, p + LPR, ...: the bucket's logits, maximum,
+//      exp terms and their sum in logit order, the action (first maximum, or
+//      the inverse-CDF draw over the terms in logit order), logit -
+//      logsumexp, into LDS;
 //   C  lane part 0: the six terms summed in bucket order, the outputs.
 // Every value is the one pol_bucket_term / pol_select computes (same
 // operations on the same inputs), so rows are bit-identical to MT = 4's.
+// (Until round 5 the maxima and the exp terms were separate phases with an
+// LDS round trip between them: 8 192-world PPO trace 0.64 + 0.48 + 0.84 us.)
 // The bucket pass's LDS exchange of one wave (R rows).
 template <int R>
 struct BucketLds {
-    float e[R][POL_LOGITS + 1], t[R][POL_BUCKETS];
+    float t[R][POL_BUCKETS];
     int32_t a[R][POL_BUCKETS];
 };
 
@@ -209,8 +210,8 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
 {
     static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
     constexpr int LPR = 64 / R;
-    constexpr int LGL = (POL_LOGITS + LPR - 1) / LPR, BPL = (POL_BUCKETS + LPR - 1) / LPR;
-    float (*ebuf)[POL_LOGITS + 1] = buf.e, (*tbuf)[POL_BUCKETS] = buf.t;
+    constexpr int BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    float (*tbuf)[POL_BUCKETS] = buf.t;
     int32_t (*abuf)[POL_BUCKETS] = buf.a;
     const int r = lane / LPR, part = lane % LPR;
     const int64_t rr = row0 + r;
@@ -223,73 +224,61 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     if constexpr (!PRE) {
         if (stochastic) bucket_noise<R>(own, a.seed, a.step, row0, a.rows, lane, a.key_row0);
     }
-    // bucket maxima (every lane, compile-time indices)
-    float mx[POL_BUCKETS];
-#pragma unroll
-    for (int b = 0; b < POL_BUCKETS; b++) {
-        const int o = pol_bucket_off(b), nb = pol_bucket(b);
-        float m = lg[o];
-        for (int i = 1; i < nb; i++) m = lg[o + i] > m ? lg[o + i] : m;
-        mx[b] = m;
-    }
-    if (ts) __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) (diagnostics)
+    // one phase per bucket: lane part p takes buckets p, p + LPR, ...: its
+    // logits (up to 8) into registers, the maximum, exp(logit - max) of each,
+    // their sum in logit order, the action (first maximum, or the inverse-CDF
+    // draw over the terms in logit order), logit[a] - (max + log(sum)) --
+    // pol_bucket_term's operations, the terms never leave the registers
     bucket_stamp(ts, 0, lane);
-#pragma unroll
-    for (int j = 0; j < LGL; j++) {
-        const int i = part + LPR * j;
-        if (i < POL_LOGITS) {
-            const int b = (i >= 2) + (i >= 10) + (i >= 13) + (i >= 15) + (i >= 17);
-            float m = mx[0];
-#pragma unroll
-            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
-            ebuf[r][i] = pol_expf(lg[i] - m);
-        }
-    }
-    pol_wave_sync();
-    bucket_stamp(ts, 1, lane);
 #pragma unroll
     for (int j = 0; j < BPL; j++) {
         const int b = part + LPR * j;
         if (b < POL_BUCKETS) {
             const int o = pol_bucket_off(b), nb = pol_bucket(b);
-            float s = ebuf[r][o];
+            float l[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) l[i] = i < nb ? lg[o + i] : 0.f;
+            float mx = l[0];
 #pragma unroll
             for (int i = 1; i < 8; i++)
-                if (i < nb) s = s + ebuf[r][o + i];
+                if (i < nb) mx = l[i] > mx ? l[i] : mx;
+            float e[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) e[i] = pol_expf(l[i] - mx);
+            float sum = e[0];
+#pragma unroll
+            for (int i = 1; i < 8; i++)
+                if (i < nb) sum = sum + e[i];
             int act = 0;
             if (stochastic) {
-                // pol_inverse_cdf over the bucket's terms, read again from LDS
-                // (the same running sums: no register copy of the terms)
                 const float u = PRE ? pre->u[j] : own.u[j];
-                const float t = u * s;
+                const float t = u * sum;
                 float cs = 0.f;
                 act = nb - 1;
 #pragma unroll
                 for (int i = 0; i < 7; i++) {
                     if (i < nb - 1) {
-                        cs = cs + ebuf[r][o + i];
+                        cs = cs + e[i];
                         if (act == nb - 1 && cs > t) act = i;
                     }
                 }
             } else {
-                float best = lg[o];
+                float best = l[0];
 #pragma unroll
                 for (int i = 1; i < 8; i++) {
-                    if (i < nb) {
-                        const float g = lg[o + i];
-                        if (g > best) { best = g; act = i; }  // first maximum
-                    }
+                    if (i < nb && l[i] > best) { best = l[i]; act = i; }  // first maximum
                 }
             }
-            float m = mx[0];
+            const float lse = mx + pol_logf(sum);
+            float la = l[0];
 #pragma unroll
-            for (int q = 1; q < POL_BUCKETS; q++) m = b == q ? mx[q] : m;
-            const float lse = m + pol_logf(s);
+            for (int i = 1; i < 8; i++) la = act == i ? l[i] : la;
             abuf[r][b] = act;
-            tbuf[r][b] = lg[o + act] - lse;
+            tbuf[r][b] = la - lse;
         }
     }
     pol_wave_sync();
+    bucket_stamp(ts, 1, lane);
     bucket_stamp(ts, 2, lane);
     if (part == 0 && live) {
         float term[POL_BUCKETS];
@@ -398,6 +387,57 @@ __device__ __forceinline__ void policy_tail_lds(const PolicyLdsWeights &L, float
     }
 }
 
+// policy_tail_lds for two M-tiles at once (rows 0..31 of t[32][33]): each
+// layer's MFMA chains of both tiles are issued before the first tile's
+// LayerNorm, so that tile's VALU work runs while the matrix pipe works
+// through the second tile's chains.  The same operations on the same values.
+__device__ __forceinline__ void policy_tail_lds2(const PolicyLdsWeights &L, float (*t)[33], int c, int q)
+{
+#pragma unroll
+    for (int layer = 0; layer < 2; layer++) {
+        const float (*wl)[32][PWG_P2] = layer == 0 ? L.w2 : L.wh;
+        float h[2][8];
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int j = 0; j < 8; j++) h[m][j] = t[16 * m + c][8 * q + j];
+        pol_wave_sync();
+        float w0[8], w1[8];
+#pragma unroll
+        for (int v = 0; v < 2; v++) {
+            const float4 u0 = *(const float4 *)&wl[q][c][4 * v];
+            const float4 u1 = *(const float4 *)&wl[q][16 + c][4 * v];
+            w0[4 * v] = u0.x; w0[4 * v + 1] = u0.y; w0[4 * v + 2] = u0.z; w0[4 * v + 3] = u0.w;
+            w1[4 * v] = u1.x; w1[4 * v + 1] = u1.y; w1[4 * v + 2] = u1.z; w1[4 * v + 3] = u1.w;
+        }
+        f32x4 a[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            a[m][0] = a[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                a[m][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(h[m][j], w0[j], a[m][0], 0, 0, 0);
+                a[m][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(h[m][j], w1[j], a[m][1], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < 2; m++) {
+            float (*tm)[33] = t + 16 * m;
+            if (layer == 0) {
+                ln_relu_to_tile(a[m][0], a[m][1], L.cst[3][c], L.cst[3][c + 16], L.cst[4][c], L.cst[4][c + 16],
+                                L.cst[5][c], L.cst[5][c + 16], tm, c, q);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    tm[4 * q + i][c] = a[m][0][i] + L.cst[6][c];
+                    tm[4 * q + i][c + 16] = a[m][1][i] + L.cst[6][c + 16];
+                }
+            }
+        }
+        pol_wave_sync();
+    }
+}
+
 // The B operands and the per-column constants of one lane, loaded once per
 // wave and kept in registers for every tile it processes.
 struct PolicyRegs {
@@ -426,6 +466,40 @@ __device__ __forceinline__ void load_policy_regs(PolicyRegs &R, const PolicyWeig
     R.b2_0 = W.b2[c]; R.b2_1 = W.b2[c + 16]; R.l2w0 = W.ln2_w[c]; R.l2w1 = W.ln2_w[c + 16];
     R.l2b0 = W.ln2_b[c]; R.l2b1 = W.ln2_b[c + 16];
     R.bh0 = W.head_b[c]; R.bh1 = W.head_b[c + 16];
+}
+
+// Layer 2 + LayerNorm + ReLU, then the heads, of one 16-row M-tile whose
+// layer-1 output is in tm[16][33] (policy_layers' second loop; the B operands
+// in registers): row r's 19 logits and value into tm[r][0..19].
+__device__ __forceinline__ void policy_tail_regs(const PolicyRegs &R, float (*tm)[33], int c, int q)
+{
+    float h[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
+    pol_wave_sync();
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[0][j], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[1][j], a1, 0, 0, 0);
+    }
+    ln_relu_to_tile(a0, a1, R.b2_0, R.b2_1, R.l2w0, R.l2w1, R.l2b0, R.l2b1, tm, c, q);
+    pol_wave_sync();
+#pragma unroll
+    for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
+    pol_wave_sync();
+    a0 = f32x4{0.f, 0.f, 0.f, 0.f};
+    a1 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[0][j], a0, 0, 0, 0);
+        a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[1][j], a1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        tm[4 * q + i][c] = a0[i] + R.bh0;
+        tm[4 * q + i][c + 16] = a1[i] + R.bh1;
+    }
 }
 
 // The network on one tile of 16 MT rows: x[m][j] = observation float 32q + j
@@ -481,36 +555,47 @@ __device__ __forceinline__ void policy_layers(float (&x)[MT][32], const PolicyRe
     pol_wave_sync();
     // layer 2 and heads, per M-tile through its 16 rows of the tile
 #pragma unroll
-    for (int m = 0; m < MT; m++) {
-        float (*tm)[33] = tile + 16 * m;
-        float h[8];
+    for (int m = 0; m < MT; m++) policy_tail_regs(R, tile + 16 * m, c, q);
+    pol_wave_sync();
+}
+
+// policy_layers<1> with the rows arriving in two halves (as
+// policy_layers_half_split): lane group q's floats 32q + [0, 16) of row c are
+// in LDS at xrow when called, 32q + [16, 32) after mid().  Layer 1's two
+// accumulator chains take steps 0..15 before mid(), 16..31 after; then the
+// LayerNorm, layer 2 and the heads of policy_layers.  The same bits.
+template <class Mid>
+__device__ __forceinline__ void policy_layers1_split(const float *xrow, const PolicyRegs &R,
+                                                     const float (*norm)[POL_IN], float (*tile)[33], int c, int q,
+                                                     Mid mid)
+{
+    f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
-        pol_wave_sync();
-        f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = {0.f, 0.f, 0.f, 0.f};
+    for (int half = 0; half < 2; half++) {
+        if (half == 1) mid();
+        float x[16];
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[0][j], a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.w2[1][j], a1, 0, 0, 0);
+        for (int v = 0; v < 4; v++) {
+            const int k = 32 * q + 16 * half + 4 * v;
+            const float4 o = *(const float4 *)(xrow + k);
+            const float4 a4 = *(const float4 *)&norm[0][k];
+            const float4 b4 = *(const float4 *)&norm[1][k];
+            x[4 * v] = pol_clamp((o.x - a4.x) * b4.x);
+            x[4 * v + 1] = pol_clamp((o.y - a4.y) * b4.y);
+            x[4 * v + 2] = pol_clamp((o.z - a4.z) * b4.z);
+            x[4 * v + 3] = pol_clamp((o.w - a4.w) * b4.w);
         }
-        ln_relu_to_tile(a0, a1, R.b2_0, R.b2_1, R.l2w0, R.l2w1, R.l2b0, R.l2b1, tm, c, q);
-        pol_wave_sync();
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < 8; j++) h[j] = tm[c][8 * q + j];
-        pol_wave_sync();
-        a0 = f32x4{0.f, 0.f, 0.f, 0.f};
-        a1 = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[0][j], a0, 0, 0, 0);
-            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[j], R.wh[1][j], a1, 0, 0, 0);
+        for (int j = 0; j < 16; j++) {
+            a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[0][16 * half + j], a0, 0, 0, 0);
+            a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[1][16 * half + j], a1, 0, 0, 0);
         }
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            tm[4 * q + i][c] = a0[i] + R.bh0;
-            tm[4 * q + i][c + 16] = a1[i] + R.bh1;
-        }
+        __builtin_amdgcn_sched_barrier(0);
     }
+    ln_relu_to_tile(a0, a1, R.b1_0, R.b1_1, R.l1w0, R.l1w1, R.l1b0, R.l1b1, tile, c, q);
+    pol_wave_sync();
+    policy_tail_regs(R, tile, c, q);
     pol_wave_sync();
 }
 
@@ -541,31 +626,13 @@ __device__ __forceinline__ void ln_relu_rows(f32x4 a0, f32x4 a1, float bias0, fl
 struct HalfExchange {
     f32x4 acc[2][64];  // [h][lane]
 };
+// The part of policy_layers_half after layer 1's chain (acc: the wave's half
+// of the M-tile's layer-1 outputs).
 template <class Bar>
-__device__ __forceinline__ void policy_layers_half(float (&x)[32], const PolicyRegs &R, const float (*norm)[POL_IN],
-                                                   float (*tile)[33], float (*ltile)[33], HalfExchange &ex, int c,
-                                                   int q, int lane, int h, Bar bar)
+__device__ __forceinline__ void policy_layers_half_rest(f32x4 acc, const PolicyRegs &R, float (*tile)[33],
+                                                        float (*ltile)[33], HalfExchange &ex, int c, int q, int lane,
+                                                        int h, Bar bar)
 {
-    float nm[32], ni[32];
-#pragma unroll
-    for (int v = 0; v < 8; v++) {
-        const float4 a4 = *(const float4 *)&norm[0][32 * q + 4 * v];
-        const float4 b4 = *(const float4 *)&norm[1][32 * q + 4 * v];
-        nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
-        ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
-    }
-#pragma unroll
-    for (int j = 0; j < 32; j++) x[j] = pol_clamp((x[j] - nm[j]) * ni[j]);
-    __builtin_amdgcn_sched_barrier(0);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    if (h == 0) {
-#pragma unroll
-        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[0][j], acc, 0, 0, 0);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[1][j], acc, 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
     ex.acc[h][lane] = acc;
     bar();
     if (h == 0)
@@ -605,6 +672,76 @@ __device__ __forceinline__ void policy_layers_half(float (&x)[32], const PolicyR
 #pragma unroll
     for (int i = 0; i < 4; i++) ltile[4 * q + i][c + 16 * h] = acc[i] + bh;
     bar();
+}
+
+template <class Bar>
+__device__ __forceinline__ void policy_layers_half(float (&x)[32], const PolicyRegs &R, const float (*norm)[POL_IN],
+                                                   float (*tile)[33], float (*ltile)[33], HalfExchange &ex, int c,
+                                                   int q, int lane, int h, Bar bar)
+{
+    float nm[32], ni[32];
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        const float4 a4 = *(const float4 *)&norm[0][32 * q + 4 * v];
+        const float4 b4 = *(const float4 *)&norm[1][32 * q + 4 * v];
+        nm[4 * v] = a4.x; nm[4 * v + 1] = a4.y; nm[4 * v + 2] = a4.z; nm[4 * v + 3] = a4.w;
+        ni[4 * v] = b4.x; ni[4 * v + 1] = b4.y; ni[4 * v + 2] = b4.z; ni[4 * v + 3] = b4.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 32; j++) x[j] = pol_clamp((x[j] - nm[j]) * ni[j]);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[0][j], acc, 0, 0, 0);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 32; j++) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[1][j], acc, 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    policy_layers_half_rest(acc, R, tile, ltile, ex, c, q, lane, h, bar);
+}
+
+// policy_layers_half with the rows arriving in two halves: lane group q's
+// floats 32q + [0, 16) are in LDS at xrow (row c of the M-tile) when called,
+// floats 32q + [16, 32) after mid() (a workgroup barrier: the hand-off of the
+// second half).  Layer 1's chain steps 0..15 run before mid(), 16..31 after --
+// the same chain, the same bits.
+template <class Mid, class Bar>
+__device__ __forceinline__ void policy_layers_half_split(const float *xrow, const PolicyRegs &R,
+                                                         const float (*norm)[POL_IN], float (*tile)[33],
+                                                         float (*ltile)[33], HalfExchange &ex, int c, int q, int lane,
+                                                         int h, Mid mid, Bar bar)
+{
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+        if (half == 1) mid();
+        float x[16];
+#pragma unroll
+        for (int v = 0; v < 4; v++) {
+            const int k = 32 * q + 16 * half + 4 * v;
+            const float4 o = *(const float4 *)(xrow + k);
+            const float4 a4 = *(const float4 *)&norm[0][k];
+            const float4 b4 = *(const float4 *)&norm[1][k];
+            x[4 * v] = pol_clamp((o.x - a4.x) * b4.x);
+            x[4 * v + 1] = pol_clamp((o.y - a4.y) * b4.y);
+            x[4 * v + 2] = pol_clamp((o.z - a4.z) * b4.z);
+            x[4 * v + 3] = pol_clamp((o.w - a4.w) * b4.w);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (h == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[0][16 * half + j], acc, 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++)
+                acc = __builtin_amdgcn_mfma_f32_16x16x4f32(x[j], R.w1[1][16 * half + j], acc, 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    policy_layers_half_rest(acc, R, tile, ltile, ex, c, q, lane, h, bar);
 }
 
 }  // namespace bb

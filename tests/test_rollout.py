@@ -217,12 +217,14 @@ def test_gpu_rollout_chunks_and_unrecorded(native_lib):
 
 
 @pytest.mark.gpu
-def test_gpu_rollout_more_agents_per_step_path(native_lib):
-    """N = 4 has no fused kernel: bb_rollout launches k_step per step."""
+@pytest.mark.parametrize("N,W,K", [(4, 700, 60), (6, 1001, 40), (8, 333, 30), (10, 777, 30)])
+def test_gpu_rollout_more_agents_fused_equals_host(native_lib, N, W, K):
+    """N >= 4: one k_rollout_shared launch for all K steps (the world in LDS,
+    rows from the source table) == the host executor, every recorded output,
+    every written-back action and every column afterwards (ragged last waves)."""
     _gpu()
-    W, K = 700, 60
-    g = make_sim(ExecMode.CUDA, W, num_agents=4, per_world_rng=True)
-    h = make_sim(ExecMode.CPU, W, num_agents=4, per_world_rng=True)
+    g = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
+    h = make_sim(ExecMode.CPU, W, num_agents=N, per_world_rng=True)
     acts = g.stage_random_actions(K, action_seed=4, step0=0)
     bg, bh = g.rollout_buffers(K), h.rollout_buffers(K)
     ag, ah = acts.clone(), acts.cpu().clone()
@@ -233,6 +235,36 @@ def test_gpu_rollout_more_agents_per_step_path(native_lib):
     for key in ("obs", "reward", "done"):
         assert_same(bg[key], bh[key], key)
     assert_same_sims(g, h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,W,K,flags", [(4, 65536, 8, dict()), (10, 8192, 12, dict()),
+                                         (4, 4096, 40, dict(one_on_one=False, tag_mask=False)),
+                                         (6, 2048, 24, dict(tag_mask=False))])
+def test_gpu_rollout_more_agents_fused_equals_per_step_launches(native_lib, N, W, K, flags):
+    """The fused N >= 4 rollout == K k_step launches (the per_step flag), bit for
+    bit, at BASELINE configs[1]'s 65 536 worlds x 4 agents and 8 192 x 10; the
+    unrecorded form (outputs None: rows, rewards, done flags into the sim's own
+    tensors every step) as well."""
+    _gpu()
+    f = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True, **flags)
+    p = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True, **flags)
+    acts = f.stage_random_actions(2 * K, action_seed=5, step0=0)
+    af, ap = acts[:K].clone(), acts[:K].clone()
+    bf, bp = f.rollout_buffers(K), p.rollout_buffers(K)
+    f.rollout(af, bf["obs"], bf["reward"], bf["done"])
+    p.rollout(ap, bp["obs"], bp["reward"], bp["done"], per_step=True)
+    torch.cuda.synchronize()
+    assert_same(af, ap, "actions")
+    for key in ("obs", "reward", "done"):
+        assert_same(bf[key], bp[key], key)
+    assert_same_sims(f, p)
+    af, ap = acts[K:].clone(), acts[K:].clone()
+    f.rollout(af)
+    p.rollout(ap, per_step=True)
+    torch.cuda.synchronize()
+    assert_same(af, ap, "actions (unrecorded)")
+    assert_same_sims(f, p)
 
 
 @pytest.mark.gpu

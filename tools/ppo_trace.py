@@ -58,9 +58,9 @@ def main():
     print(f"  S: systems {pct(ns(0, 1))}; row sources {pct(ns(1, 20))}; X free + pass 0 {pct(ns(20, 21))}; "
           f"pass 1 (+ last-step rows) {pct(ns(21, 2))}")
     # P (first policy wave), pass of step k + 1 against S's rows of step k
-    names = [(4, 6, "layer 1, steps 0-15"), (6, 7, "wait: rows' second half"), (7, 8, "layer 1, steps 16-31 (+bar)"),
-             (8, 9, "LN 1 (+bar)"), (9, 10, "layer 2 (+bar)"), (10, 11, "LN 2 (+bar)"), (11, 12, "heads (+bar)"),
-             (12, 13, "bucket maxima"), (13, 14, "bucket per-logit"), (14, 15, "bucket per-bucket"),
+    names = [(4, 6, "layer 1, steps 0-15"), (6, 7, "wait: rows' second half"),
+             (7, 12, "layer 1 steps 16-31, LN 1, layer 2, LN 2, heads"),
+             (12, 13, "bucket: uniforms (drawn ahead: 0)"), (13, 14, "bucket per-bucket"),
              (15, 16, "bucket outputs"), (16, 3, "to actions")]
     print("  P: " + "; ".join(f"{n} {pct(ns(i, j, slice(1, None)))}" for i, j, n in names))
     # the overlap: P's layer 1 on pass 0 of step k's rows starts before S has
