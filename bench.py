@@ -371,7 +371,8 @@ def main():
             line = {"worlds": W2 * world_size, "worlds_per_gpu": W2, "n_gpus": world_size, "agents": n2,
                     "steps": steps2, "value": W2 * world_size * steps2 / wall2, "unit": "env-steps/s",
                     "ms_per_step": wall2 * 1e3 / steps2,
-                    "kernel": ("bb::k_rollout<%d>" if fused2 else "bb::k_step<%d>") % n2,
+                    "kernel": (("bb::k_rollout<%d>" if n2 == 2 else "bb::k_rollout_shared<%d>") if fused2
+                               else "bb::k_step<%d>") % n2,
                     "launches_timed": launches, "kernel_avg_us": k2 * 1e6,
                     "kernel_us_per_step": k2 * 1e6 / (K2 or 1), "achieved": b2 / k2 / 1e9,
                     "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(key),
@@ -433,6 +434,9 @@ def main():
             extra["config_c2_8192x2_rollout32"] = config_line(8192, 2, 32, launches=EVENT_MIN_LAUNCHES // 4)
             extra["config_c4_shard_32768x2"] = config_line(32768, 2)
             extra["config_2v2_65536x4"] = config_line(65536, 4)
+            # the "2v2" configuration as K = 32 rollouts (one k_rollout_shared
+            # launch per 32 steps; 8 launches: the staged actions are 6 MB a step)
+            extra["config_2v2_65536x4_rollout32"] = config_line(65536, 4, 32, launches=8)
             extra["config_c5_65536x10"] = config_line(65536, 10)
             extra["ppo_rollout32_8192x2"] = ppo_line(8192)
             extra["ppo_rollout32_65536x2"] = ppo_line(65536)

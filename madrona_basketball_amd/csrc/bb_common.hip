@@ -371,8 +371,25 @@ bool step_records(int n)
     }
 }
 
+// The K-step rollout kernel at N >= 4 agents (k_rollout_shared: the world in
+// LDS across the steps) is taken up to this many agents.  At N = 4 it keeps
+// 1/4 of the world's words per lane in registers across the row pass and
+// beats per-step launches (65 536 worlds: 45.3 vs 62.7 us per step); from
+// N = 6 the row-source table sits beside the world instead (the register copy
+// spills), which costs occupancy: N = 10 396 vs 290 us per step
+// (profiles/r05/g_*, h_*).  MADRONA_BB_ROLLOUT_SHARED_MAX_N overrides it.
+static int rollout_shared_max_n()
+{
+    static const int v = [] {
+        const char *e = getenv("MADRONA_BB_ROLLOUT_SHARED_MAX_N");
+        return e && *e ? atoi(e) : 4;
+    }();
+    return v;
+}
+
 bool fused_rollout_n(int n)
 {
+    if (n >= 4 && n > rollout_shared_max_n()) return false;
     switch (n) {
     case 2: return fused_rollout<2>();
     case 4: return fused_rollout<4>();

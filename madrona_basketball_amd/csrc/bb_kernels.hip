@@ -151,15 +151,21 @@ struct Lanes {
 #define BB_OBS_PHASE_PIECES 15  // at most this many 16-byte pieces of a row per pass
 #endif
 // ALIGN: row writes end on this byte boundary (zero pieces added);
-// MAXP: at most this many 16-byte pieces of a row per pass.
-template <int N, int ALIGN = BB_OBS_WRITE_ALIGN, int MAXP = BB_OBS_PHASE_PIECES, int STORE_AUX = BB_STEP_AUX>
+// MAXP: at most this many 16-byte pieces of a row per pass; ROUND: a pass
+// holds a multiple of this many pieces (4: passes split rows on 64-byte
+// segment boundaries; diagnostic variants).
+#ifndef BB_OBS_PHASE_ROUND
+#define BB_OBS_PHASE_ROUND 1
+#endif
+template <int N, int ALIGN = BB_OBS_WRITE_ALIGN, int MAXP = BB_OBS_PHASE_PIECES, int STORE_AUX = BB_STEP_AUX,
+          int ROUND = BB_OBS_PHASE_ROUND>
 struct PhasedTile {
     static constexpr int AUX = STORE_AUX;  // cache policy of the row stores (row_store)
     static constexpr int QU = (obs_used(N) + 3) / 4;  // pieces holding row values
     static constexpr int QA = (QU * 16 + ALIGN - 1) / ALIGN * ALIGN / 16;
     static constexpr int QW = QA < obs_width(N) / 4 ? QA : obs_width(N) / 4;  // pieces written
     static constexpr int PH = (QW + MAXP - 1) / MAXP;
-    static constexpr int QP = (QW + PH - 1) / PH;
+    static constexpr int QP = ((QW + PH - 1) / PH + ROUND - 1) / ROUND * ROUND;
     static constexpr int RS = QP * 4 + (QP % 2 == 0 ? 4 : 0);  // == 4 mod 8 dwords
     static constexpr int FLOATS = WAVE * RS;
 };
@@ -177,7 +183,7 @@ struct PhasedTile {
 #define BB_LINES_MAXP 16
 #endif
 template <int N>
-using RolloutTile = PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_ROLLOUT_AUX>;
+using RolloutTile = PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_ROLLOUT_AUX, 1>;
 
 // k_step's tile.  LINES (state beyond the Infinity Cache): whole 128-byte
 // lines per pass, zero tail included, like k_rollout -- at 262 144 worlds
@@ -185,7 +191,7 @@ using RolloutTile = PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_ROLLOUT_AUX>
 // otherwise 2 x 13 pieces (416 written bytes per row), cheaper while the rows
 // stay cache-resident (65 536 worlds: 21.95 vs 22.14 us).
 template <int N, bool LINES>
-using StepTile = typename std::conditional<LINES, PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_LINES_AUX>, PhasedTile<N>>::type;
+using StepTile = typename std::conditional<LINES, PhasedTile<N, BB_LINES_ALIGN, BB_LINES_MAXP, BB_LINES_AUX, 1>, PhasedTile<N>>::type;
 
 // RowSink restricted to floats [LO, HI) of the row; `row` points at float LO.
 // Indices are compile-time after unrolling, so the window test folds away and
@@ -1309,6 +1315,16 @@ constexpr int PPS_RS = 60;  // tile row stride (floats): 14 pieces + 1, == 4 mod
 #ifndef BB_PPS_REC_AUX
 #define BB_PPS_REC_AUX 16
 #endif
+// Timing variants of k_step_ppo (identical results): BB_PPS_EARLY_BAR = 1
+// publishes the workgroup's weights with a barrier right after the state
+// loads (the waves are aligned there anyway) instead of after pass 0's rows;
+// BB_PPS_FLUSH_FIRST = 1 issues a pass's row stores before its MFMAs.
+#ifndef BB_PPS_EARLY_BAR
+#define BB_PPS_EARLY_BAR 0
+#endif
+#ifndef BB_PPS_FLUSH_FIRST
+#define BB_PPS_FLUSH_FIRST 0
+#endif
 constexpr int PPS_TILE = WAVE * PPS_RS;
 
 template <int WPG>
@@ -1517,6 +1533,7 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     pps_trace(a, gw, 1, true);
     // the workgroup's copy of the network (read after the barrier below)
     if (!skew) policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
+    if (BB_PPS_EARLY_BAR && !skew) lds_barrier();
     if (active) step_world_pre_obs(s, c, ag);
     pps_trace(a, gw, 2);
     if (active) {
@@ -1550,18 +1567,20 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     wave_sync();  // the parked words are read
     ppo_emit_pass<0>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
-    if (!skew) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
+    if (!skew && !BB_PPS_EARLY_BAR) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
     else wave_sync();
     pps_trace(a, gw, 4);
+    if (BB_PPS_FLUSH_FIRST) ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     if (!(diag & 4u)) ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
-    ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
+    if (!BB_PPS_FLUSH_FIRST) ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
     pps_trace(a, gw, 5);
     ppo_emit_pass<1>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
     wave_sync();
     pps_trace(a, gw, 6);
+    if (BB_PPS_FLUSH_FIRST) ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     if (!(diag & 4u)) ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
-    ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
+    if (!BB_PPS_FLUSH_FIRST) ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
     pps_trace(a, gw, 7);
     if (LAST && !a.value) return;  // (wave-uniform; no barrier follows)

@@ -216,13 +216,7 @@ def test_gpu_rollout_chunks_and_unrecorded(native_lib):
     assert int(torch.count_nonzero(b.observations_tensor().to_torch()[..., used:])) == 0
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("N,W,K", [(4, 700, 60), (6, 1001, 40), (8, 333, 30), (10, 777, 30)])
-def test_gpu_rollout_more_agents_fused_equals_host(native_lib, N, W, K):
-    """N >= 4: one k_rollout_shared launch for all K steps (the world in LDS,
-    rows from the source table) == the host executor, every recorded output,
-    every written-back action and every column afterwards (ragged last waves)."""
-    _gpu()
+def more_agents_fused_equals_host(N, W, K):
     g = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
     h = make_sim(ExecMode.CPU, W, num_agents=N, per_world_rng=True)
     acts = g.stage_random_actions(K, action_seed=4, step0=0)
@@ -237,16 +231,7 @@ def test_gpu_rollout_more_agents_fused_equals_host(native_lib, N, W, K):
     assert_same_sims(g, h)
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("N,W,K,flags", [(4, 65536, 8, dict()), (10, 8192, 12, dict()),
-                                         (4, 4096, 40, dict(one_on_one=False, tag_mask=False)),
-                                         (6, 2048, 24, dict(tag_mask=False))])
-def test_gpu_rollout_more_agents_fused_equals_per_step_launches(native_lib, N, W, K, flags):
-    """The fused N >= 4 rollout == K k_step launches (the per_step flag), bit for
-    bit, at BASELINE configs[1]'s 65 536 worlds x 4 agents and 8 192 x 10; the
-    unrecorded form (outputs None: rows, rewards, done flags into the sim's own
-    tensors every step) as well."""
-    _gpu()
+def more_agents_fused_equals_per_step(N, W, K, flags):
     f = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True, **flags)
     p = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True, **flags)
     acts = f.stage_random_actions(2 * K, action_seed=5, step0=0)
@@ -287,3 +272,46 @@ def test_gpu_fused_rollout_full_size_identical_worlds(native_lib):
     for name, v in sim._views.items():
         flat = v.reshape(W, -1).view(torch.int32) if v.dim() > 1 else v.view(torch.int32)[:, None]
         assert torch.equal(flat, flat[:1].expand_as(flat)), name
+
+
+# The N >= 4 K-step rollout kernel (k_rollout_shared) is the default up to
+# MADRONA_BB_ROLLOUT_SHARED_MAX_N agents (4; read once per process): the cases
+# run in a child process with the bound at 10, so every N takes the kernel.
+MORE_AGENTS_CHILD = r"""
+import torch
+from tests.test_rollout import more_agents_fused_equals_host, more_agents_fused_equals_per_step
+for N, W, K in [(4, 700, 60), (6, 1001, 40), (8, 333, 30), (10, 777, 30)]:
+    more_agents_fused_equals_host(N, W, K)
+for N, W, K, flags in [(4, 65536, 8, dict()), (10, 8192, 12, dict()),
+                       (4, 4096, 40, dict(one_on_one=False, tag_mask=False)), (6, 2048, 24, dict(tag_mask=False))]:
+    more_agents_fused_equals_per_step(N, W, K, flags)
+print("MORE_AGENTS_OK")
+"""
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_more_agents_fused(native_lib):
+    """N >= 4: one k_rollout_shared launch for all K steps (the world in LDS,
+    rows from the source table) == the host executor (ragged last waves) and ==
+    K k_step launches (the per_step flag) at BASELINE configs[1]'s 65 536 worlds
+    x 4 agents and 8 192 x 10, every recorded output, every written-back action
+    and every column afterwards; the unrecorded form (rows, rewards and done
+    flags into the sim's own tensors every step) as well."""
+    import os
+    import subprocess
+    import sys
+    _gpu()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MADRONA_BB_ROLLOUT_SHARED_MAX_N="10", PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", MORE_AGENTS_CHILD], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "MORE_AGENTS_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.gpu
+def test_gpu_rollout_more_agents_default_path(native_lib):
+    """With the default bound (fused up to 4 agents) N = 4 and N = 10 rollouts
+    still equal the host executor."""
+    _gpu()
+    more_agents_fused_equals_host(4, 700, 20)
+    more_agents_fused_equals_host(10, 333, 12)
