@@ -354,6 +354,11 @@ hipError_t launch_rollout_policy(int n, const Params &p, const PolicyRolloutArgs
 }
 
 hipError_t launch_step_ppo_2(const Params &p, const PpoStepArgs &a, hipStream_t s);  // bb_kernels.hip (N = 2)
+hipError_t launch_rollout_ppo_2(const Params &p, const PpoStepArgs &a, int32_t steps, hipStream_t s);
+hipError_t launch_rollout_ppo(int n, const Params &p, const PpoStepArgs &a, int32_t steps, hipStream_t s)
+{
+    return n == 2 ? launch_rollout_ppo_2(p, a, steps, s) : hipErrorNotSupported;
+}
 hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s)
 {
     return n == 2 ? launch_step_ppo_2(p, a, s) : hipErrorNotSupported;

@@ -1001,6 +1001,17 @@ static int64_t ppo_fused_max_worlds()
 // PPO's loop as one k_step_ppo launch per step (the trainee's policy pass fused
 // behind the world step, its rows read from LDS) from this many worlds on;
 // MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never).
+// The fused step's rollout as one k_rollout_ppo launch (default) or as one
+// k_step_ppo launch per step (MADRONA_BB_PPO_STEP_LOOP=0; bit-identical).
+static bool ppo_step_loop()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("MADRONA_BB_PPO_STEP_LOOP");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+
 static int64_t ppo_step_fused_min_worlds()
 {
     static const int64_t v = [] {
@@ -1152,7 +1163,26 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         uint64_t *ts = nullptr;
         if (trace && *trace && hipMalloc(&ts, (size_t)n * waves * bb::PPS_TRACE_POINTS * 8) != hipSuccess) ts = nullptr;
         hipError_t e = bb::launch_policy(pass(0, false), st);
-        for (int32_t k = 0; k < n && e == hipSuccess; k++) {
+        if (e == hipSuccess && ppo_step_loop()) {
+            // the whole rollout in one k_rollout_ppo launch
+            bb::PpoStepArgs a{};
+            a.diag = diag;
+            a.diag_ts = ts;
+            a.w = policy_weights(w);
+            a.trainee = trainee; a.stochastic = stochastic ? 1 : 0; a.seed = seed;
+            a.step = step0 + 1u;
+            a.reward = out->reward;
+            a.done = out->done;
+            if (n > 1) {
+                a.obs_rec = out->obs ? out->obs + W * bb::POL_IN : nullptr;
+                a.act_out = out->actions ? out->actions + W * 6 : nullptr;
+                a.log_prob = out->log_prob ? out->log_prob + W : nullptr;
+                a.value = out->value ? out->value + W : nullptr;
+            }
+            a.value_last = out->next_value;
+            e = bb::launch_rollout_ppo(s->n, s->p, a, n, st);
+        }
+        for (int32_t k = 0; k < (ppo_step_loop() ? 0 : n) && e == hipSuccess; k++) {
             bb::PpoStepArgs a{};
             a.diag = diag;
             a.diag_ts = ts ? ts + (size_t)k * waves * bb::PPS_TRACE_POINTS : nullptr;
@@ -1593,11 +1623,12 @@ int64_t bb_rollout_policy_bytes(const bb_sim *s, int32_t with_opponent, uint32_t
         // step the policy's records and the step's reward / done
         return B + (int64_t)n * (rec + outs + rd) + 4;
     case BB_PPO_PATH_FUSED_STEP:
-        // steps 0..n-2: the world step without the trainee's sim row, its row
-        // into buffer.obs[k+1], the action row into the sim, the outputs, the
+        // steps 0..n-2: the world step without sim rows (neither agent's is
+        // read before the last step rewrites them), the trainee's row into
+        // buffer.obs[k+1], the action row into the sim, the outputs, the
         // reward / done; the last step: the whole world step, reward / done,
         // next_value
-        return pass0 + (int64_t)(n - 1) * (B - row + rec + 24 + outs + rd) + B + rd + 4;
+        return pass0 + (int64_t)(n - 1) * (B - 2 * row + rec + 24 + outs + rd) + B + rd + 4;
     default:
         // per step: the world step (the trainee's row into buffer.obs[k+1]
         // instead of the sim from step 0 to n-2), then a policy pass reading

@@ -1315,16 +1315,6 @@ constexpr int PPS_RS = 60;  // tile row stride (floats): 14 pieces + 1, == 4 mod
 #ifndef BB_PPS_REC_AUX
 #define BB_PPS_REC_AUX 16
 #endif
-// Timing variants of k_step_ppo (identical results): BB_PPS_EARLY_BAR = 1
-// publishes the workgroup's weights with a barrier right after the state
-// loads (the waves are aligned there anyway) instead of after pass 0's rows;
-// BB_PPS_FLUSH_FIRST = 1 issues a pass's row stores before its MFMAs.
-#ifndef BB_PPS_EARLY_BAR
-#define BB_PPS_EARLY_BAR 0
-#endif
-#ifndef BB_PPS_FLUSH_FIRST
-#define BB_PPS_FLUSH_FIRST 0
-#endif
 constexpr int PPS_TILE = WAVE * PPS_RS;
 
 template <int WPG>
@@ -1408,27 +1398,27 @@ __device__ __forceinline__ void ppo_layer1_pass(const float *tile, const PolicyL
 }
 
 // Stores of pass P: tile piece t of row r is row piece 8 (t >> 2) + 4P + (t & 3).
-// Sim rows (the non-trainee's; every row when ALL): the pass's NS pieces of
-// the 64 rows.  Record rows (buffer.obs, the trainee's): 16 pieces per pass,
-// the zero tail included, at rec + m * 512.  Rows of worlds past the grid's
-// end (bit clear in `live`) store nothing.
+// Sim rows (ALL, the last step: every row): the pass's NS pieces of the 64
+// rows.  Before the last step no sim row is stored: the trainee's goes to
+// buffer.obs only, and the other agent's is read by nobody before the last
+// step rewrites it (no opponent policy on this path; 27 MB per step at 65 536
+// worlds).  Record rows (buffer.obs, the trainee's): 16 pieces per pass, the
+// zero tail included, at rec + m * 512.  Rows of worlds past the grid's end
+// (bit clear in `live`) store nothing.
 template <int P, bool ALL>
 __device__ __forceinline__ void ppo_flush_pass(const float *tile, char *obs, char *rec, uint64_t live, int trainee,
                                                int lane)
 {
     constexpr int NS = P == 0 ? 14 : 12;
-    constexpr int NR = ALL ? WAVE : WAVE / 2;  // sim rows stored
-    constexpr int SIT = NR * NS / WAVE;        // store instructions (14 / 12 or 7 / 6)
-    static_assert(NR * NS % WAVE == 0, "whole store instructions");
+    constexpr int SIT = NS;  // store instructions: 64 rows x NS pieces
     constexpr int OWB = 128 * 4;
-    {
+    if constexpr (ALL) {
         vf4 v[SIT];
         uint32_t off[SIT];
         bool ok[SIT];
 #pragma unroll
         for (int i = 0; i < SIT; i++) {
-            const int f = i * WAVE + lane, rr = f / NS, t = f - rr * NS;
-            const int r = ALL ? rr : 2 * rr + (1 - trainee);
+            const int f = i * WAVE + lane, r = f / NS, t = f - r * NS;
             ok[i] = (live >> r) & 1ull;
             off[i] = (uint32_t)(r * OWB + (8 * (t >> 2) + 4 * P + (t & 3)) * 16);
             v[i] = *(const vf4 *)(tile + r * PPS_RS + 4 * t);
@@ -1486,34 +1476,55 @@ __device__ __forceinline__ void pps_trace(const PpoStepArgs &a, int64_t gw, int 
     }
 }
 
-template <int WPG, bool LAST>
-__device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs &a, PpoStepLds<WPG> &S, int wave,
-                                              int lane)
+// Step k of a k_rollout_ppo launch: a0 holds step 0's outputs (reward /
+// done [k], buffer.obs / actions / log_probs / values [k + 1]); the last step
+// writes next_value (a0.value_last) and no buffer entries of step k + 1.
+__device__ __forceinline__ PpoStepArgs ppo_loop_args(const PpoStepArgs &a0, int32_t k, int32_t steps, int64_t W,
+                                                     int64_t waves)
+{
+    PpoStepArgs a = a0;
+    const int64_t o = (int64_t)k * W;
+    if (a.reward) {
+        a.reward += o;
+        a.done += o;
+    }
+    a.step = a0.step + (uint32_t)k;
+    a.last = k + 1 == steps ? 1 : 0;
+    if (a.last) {
+        a.obs_rec = nullptr;
+        a.act_out = nullptr;
+        a.log_prob = nullptr;
+        a.value = a0.value_last;
+    } else {
+        if (a.obs_rec) a.obs_rec += o * POL_IN;
+        if (a.act_out) a.act_out += o * 6;
+        if (a.log_prob) a.log_prob += o;
+        if (a.value) a.value += o;
+    }
+    if (a.diag_ts) a.diag_ts += (int64_t)k * waves * PPS_TRACE_POINTS;
+    return a;
+}
+
+// LOOP: a step of k_rollout_ppo's loop (the weights are in LDS already; no
+// workgroup barrier, the waves run their worlds' steps independently).
+template <int WPG, bool LAST, bool LOOP = false>
+__device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs &a, PpoStepLds<WPG> &S, int blk,
+                                              int wave, int lane)
 {
     constexpr int N = 2;
     float *tile = S.tile[wave];
     const int k = lane % N;
-    const int64_t w0 = ((int64_t)blockIdx.x * WPG + wave) * (WAVE / N);
+    const int64_t w0 = ((int64_t)blk * WPG + wave) * (WAVE / N);
     const int64_t w = w0 + lane / N;
     const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
     const int trainee = a.trainee;
     const LaneAgents<N, MODE_FULL> ag{k, &p};
 
-    const int64_t gw = (int64_t)blockIdx.x * WPG + wave;
+    const int64_t gw = (int64_t)blk * WPG + wave;
     World<N> s;
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;
     pps_trace(a, gw, 0);
-    // (timing experiment, PpoStepArgs::diag bits 8-15: the upper half of the
-    // workgroup's waves -- one of the two waves of each SIMD -- starts that
-    // many s_sleep(127) later, the weights copied and published first)
-    const uint32_t skew = (a.diag >> 8) & 0xFFu;
-    if (skew) {
-        policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
-        lds_barrier();
-        if (wave >= WPG / 2)
-            for (uint32_t i = 0; i < skew; i++) __builtin_amdgcn_s_sleep(127);
-    }
     if (active) {
         load_world(s, p, w);
         {
@@ -1532,8 +1543,7 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     if (!LAST && a.stochastic) bucket_noise<32>(noise, a.seed, a.step, w0, p.num_worlds, lane);
     pps_trace(a, gw, 1, true);
     // the workgroup's copy of the network (read after the barrier below)
-    if (!skew) policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
-    if (BB_PPS_EARLY_BAR && !skew) lds_barrier();
+    if (!LOOP) policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
     if (active) step_world_pre_obs(s, c, ag);
     pps_trace(a, gw, 2);
     if (active) {
@@ -1567,20 +1577,18 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     for (int i = 0; i < 2; i++) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     wave_sync();  // the parked words are read
     ppo_emit_pass<0>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
-    if (!skew && !BB_PPS_EARLY_BAR) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
+    if (!LOOP) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
     else wave_sync();
     pps_trace(a, gw, 4);
-    if (BB_PPS_FLUSH_FIRST) ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     if (!(diag & 4u)) ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
-    if (!BB_PPS_FLUSH_FIRST) ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
+    ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
     pps_trace(a, gw, 5);
     ppo_emit_pass<1>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
     wave_sync();
     pps_trace(a, gw, 6);
-    if (BB_PPS_FLUSH_FIRST) ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     if (!(diag & 4u)) ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
-    if (!BB_PPS_FLUSH_FIRST) ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
+    ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
     pps_trace(a, gw, 7);
     if (LAST && !a.value) return;  // (wave-uniform; no barrier follows)
@@ -1628,7 +1636,42 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void k_step_ppo(const Params p, cons
     if constexpr (BB_N == 2) {
         __shared__ PpoStepLds<WPG> S;
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-        ppo_step_wave<WPG, LAST>(p, a, S, wave, (int)threadIdx.x % WAVE);
+        ppo_step_wave<WPG, LAST>(p, a, S, (int)blockIdx.x, wave, (int)threadIdx.x % WAVE);
+    }
+}
+
+// k_rollout_ppo<2>: the steps of k_step_ppo for a whole rollout in one launch.
+// Worlds are independent, so each wave runs its 32 worlds' K steps back to
+// back -- the state stored at the end of a step and loaded at the start of
+// the next, the trainee's actions through the sim's action column, as between
+// k_step_ppo launches -- with no kernel boundary between steps and no
+// barrier: waves drift apart, and the policy's MFMA phase of one overlaps
+// another's systems.  A wave reads only what its own lanes wrote (same wave,
+// same vector L1: coherent; the fence orders the store and the loads).  Each
+// step computes exactly what k_step_ppo computes (bit-identical).
+template <int WPG>
+__global__ __launch_bounds__(WAVE * WPG, 2) void k_rollout_ppo(const Params p, const PpoStepArgs a0, int32_t steps)
+{
+    if constexpr (BB_N == 2) {
+        __shared__ PpoStepLds<WPG> S;
+        const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        const int lane = (int)threadIdx.x % WAVE;
+        policy_weights_to_lds(S.wt, a0.w, (int)threadIdx.x, WPG * WAVE);
+        lds_barrier();
+        const int64_t W = p.num_worlds, waves = (W + WAVE / 2 - 1) / (WAVE / 2);
+        for (int32_t k = 0; k < steps; k++) {
+            // opaque per-step copies of the indices: nothing derived from them
+            // (column addresses, the world's keys) is computed before the loop
+            // and held across it
+            int32_t k_t = k, blk_t = (int)blockIdx.x, wave_t = wave, lane_t = lane;
+            __asm__ volatile("" : "+s"(k_t), "+s"(blk_t), "+s"(wave_t));
+            __asm__ volatile("" : "+v"(lane_t));
+            const PpoStepArgs a = ppo_loop_args(a0, k_t, steps, W, waves);
+            if (k_t + 1 < steps) ppo_step_wave<WPG, false, true>(p, a, S, blk_t, wave_t, lane_t);
+            else ppo_step_wave<WPG, true, true>(p, a, S, blk_t, wave_t, lane_t);
+            // this step's state / action stores before the next step's loads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        }
     }
 }
 
@@ -2554,9 +2597,26 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
 }
 
 #if BB_N == 2
-// k_step_ppo: 8-wave workgroups (the weights' 32.6 KB shared by 256 worlds,
-// 155 KB of LDS: one workgroup and 2 waves per SIMD per CU) while the grid
-// fills the device with them, 4-wave workgroups below that.
+// k_rollout_ppo / k_step_ppo: 8-wave workgroups (the weights' 32.6 KB shared
+// by 256 worlds, 155 KB of LDS: one workgroup and 2 waves per SIMD per CU)
+// while the grid fills the device with them, 4-wave workgroups below that.
+hipError_t launch_rollout_ppo_2(const Params &p, const PpoStepArgs &a, int32_t steps, hipStream_t s)
+{
+    const int64_t waves = (p.num_worlds + WAVE / 2 - 1) / (WAVE / 2);
+    const int64_t cus = device_cus();
+    // the largest workgroup whose grid still gives every CU one
+    const int wpg = waves >= 8 * cus ? 8 : waves >= 4 * cus ? 4 : waves >= 2 * cus ? 2 : 1;
+    const dim3 grid((unsigned)((waves + wpg - 1) / wpg)), block(WAVE * wpg);
+    if (steps < 1) return hipSuccess;
+    switch (wpg) {
+    case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_ppo<8>), grid, block, 0, s, p, a, steps); break;
+    case 4: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_ppo<4>), grid, block, 0, s, p, a, steps); break;
+    case 2: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_ppo<2>), grid, block, 0, s, p, a, steps); break;
+    default: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_ppo<1>), grid, block, 0, s, p, a, steps); break;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_step_ppo_2(const Params &p, const PpoStepArgs &a, hipStream_t s)
 {
     const int64_t waves = (p.num_worlds + WAVE / 2 - 1) / (WAVE / 2);

@@ -61,6 +61,7 @@ struct PpoStepArgs {
     int32_t trainee, stochastic;
     int32_t last;               // the rollout's last step: every row into the sim's obs, value only
     uint32_t seed, step;        // the policy's sampling key (seed, step0 + k + 1)
+    float *value_last;          // k_rollout_ppo: next_value (the value output of its last step)
     // diagnostics only (timing attribution; the outputs are then wrong):
     // diag bit 0 no bucket pass, 1 no LayerNorm-1 / layer 2 / heads, 2 no
     // layer-1 MFMAs, 3 no buffer.obs stores; diag_ts: PPS_TRACE_POINTS clocks
@@ -71,6 +72,10 @@ struct PpoStepArgs {
 constexpr int PPS_TRACE_POINTS = 12;
 // N = 2 only (hipErrorNotSupported otherwise)
 hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s);
+// The `steps` steps of a rollout in one launch (k_rollout_ppo<2>): `a` holds
+// step 0's arguments (outputs of step k at k x W past them; its `last` is
+// ignored), value_last the next_value output.  N = 2 only.
+hipError_t launch_rollout_ppo(int n, const Params &p, const PpoStepArgs &a, int32_t steps, hipStream_t s);
 
 // Trajectory recorder (bb_record): NSEG column segments per recorded world.
 constexpr int RECORD_SEGS = 10;

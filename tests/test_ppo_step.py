@@ -1,6 +1,8 @@
-"""k_step_ppo<2>: PPO's rollout loop as one launch per step, the trainee's
+"""k_rollout_ppo<2> / k_step_ppo<2>: PPO's rollout loop with the trainee's
 policy pass fused behind the world step (bb_rollout_policy from 32 768 worlds;
-scripts/ppo.py:65-134 over scripts/env.py:126-170).  Every recorded output
+scripts/ppo.py:65-134 over scripts/env.py:126-170), the whole rollout in one
+launch (each wave steps its worlds K times; default) or one launch per step
+(MADRONA_BB_PPO_STEP_LOOP=0, child process).  Every recorded output
 (buffer.obs / actions / log_probs / values / rewards / not_dones, next_value)
 and every simulator column must equal the per-step launches (k_policy +
 k_step, the `per_step` flag) and the loop of FusedPolicy.act + step, bit for
@@ -45,8 +47,8 @@ def fused_vs_per_step(W, n, trainee, stochastic, seed=7, step0=3, partial=False)
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,n,trainee,stochastic", [(65536, 6, 0, True), (65536, 5, 1, False),
-                                                    (32768, 8, 1, True), (40001, 4, 0, True),
-                                                    (131072, 3, 0, False)])
+                                                    (65536, 32, 1, True), (32768, 8, 1, True),
+                                                    (40001, 4, 0, True), (131072, 3, 0, False)])
 def test_gpu_fused_ppo_step_equals_per_step_launches(native_lib, W, n, trainee, stochastic):
     assert torch.cuda.is_available()
     b = fused_vs_per_step(W, n, trainee, stochastic)
@@ -91,6 +93,25 @@ def test_gpu_fused_ppo_step_forced_on_small_grids(native_lib):
                PYTHONPATH=ROOT)
     r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=env, capture_output=True, text=True,
                        timeout=240)
+    assert r.returncode == 0 and "PPO_STEP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+STEP_LAUNCHES_CHILD = r'''
+import torch
+from tests.test_ppo_step import fused_vs_per_step
+for W, n, trainee, stoch in [(65536, 6, 1, True), (40001, 4, 0, True), (65536, 1, 0, False)]:
+    fused_vs_per_step(W, n, trainee, stoch)
+print("PPO_STEP_OK")
+'''
+
+
+@pytest.mark.gpu
+def test_gpu_fused_ppo_step_one_launch_per_step(native_lib):
+    """MADRONA_BB_PPO_STEP_LOOP=0: one k_step_ppo launch per step, equal to the
+    per-step launches (and so to the one-launch rollout)."""
+    env = dict(os.environ, MADRONA_BB_PPO_STEP_LOOP="0", PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", STEP_LAUNCHES_CHILD], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
     assert r.returncode == 0 and "PPO_STEP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 

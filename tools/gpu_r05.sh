@@ -6,10 +6,11 @@
 #   bench                      default bench line (all configs, CPU baselines)
 #   prof:<W>:<N>               kernel stats of k_step<N> at W worlds, that workload alone
 #   profppo:<W>                kernel stats of the PPO rollout (K=32) at W worlds
-#   profro:<W>:<K>             kernel stats of bb_rollout (K steps per launch) at W worlds
+#   profro:<W>:<K>[:<N>]       kernel stats of bb_rollout (K steps per launch) at W worlds (N agents)
 #   pmc:<W>:<N>                FETCH_SIZE / WRITE_SIZE of k_step<N> (two passes)
 #   pmcppo:<W>                 FETCH_SIZE / WRITE_SIZE of the PPO rollout's kernels
-#   pmcro:<W>:<K>              FETCH_SIZE / WRITE_SIZE of bb_rollout
+#   pmcro:<W>:<K>[:<N>]        FETCH_SIZE / WRITE_SIZE of bb_rollout
+#   sqppo:<W>                  SQ counters of the PPO rollout's kernels (K=32)
 #   sq:<W>:<N>                 SQ issue / wait / instruction counters of k_step<N>
 #   tests                      pytest -m gpu
 #   pytest:<file>[:<k expr>]   pytest -m gpu of one test file (optionally -k)
@@ -38,7 +39,8 @@ step() {  # name timeout cmd...
 SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU"
 
 for s in "$@"; do
-    IFS=: read -r kind a b <<< "$s"
+    IFS=: read -r kind a b c <<< "$s"
+    n=${c:-2}; sfx=${c:+_N$c}
     case $kind in
     bench) step bench 600 python3 "$R/bench.py" --steps 1000 --warmup 100 ;;
     tests) step pytest_gpu 900 python3 -u -m pytest "$R/tests" -m gpu -q -rfE --timeout 300 --timeout-method thread ;;
@@ -52,8 +54,8 @@ for s in "$@"; do
             -- $B --worlds "$a" --agents "$b" --steps 300 --warmup 30 ;;
     profppo) step "prof_ppo_W$a" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ppo_W$a" -o run --output-format csv \
             -- $B --worlds "$a" --policy --rollout 32 --steps 320 --warmup 32 ;;
-    profro) step "prof_ro_W${a}_R$b" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ro_W${a}_R$b" -o run \
-            --output-format csv -- $B --worlds "$a" --rollout "$b" --steps $((16 * b)) --warmup "$b" ;;
+    profro) step "prof_ro_W${a}_R$b$sfx" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ro_W${a}_R$b$sfx" -o run \
+            --output-format csv -- $B --worlds "$a" --agents "$n" --rollout "$b" --steps $((16 * b)) --warmup "$b" ;;
     pmc) for c in FETCH_SIZE WRITE_SIZE; do
             step "pmc_W${a}_N${b}_$c" 120 rocprofv3 --pmc $c -d "$OUT/pmc_W${a}_N${b}_$c" -o run --output-format csv \
                 -- $B --worlds "$a" --agents "$b" --steps 20 --warmup 5
@@ -62,10 +64,12 @@ for s in "$@"; do
             step "pmc_ppo_W${a}_$c" 120 rocprofv3 --pmc $c -d "$OUT/pmc_ppo_W${a}_$c" -o run --output-format csv \
                 -- $B --worlds "$a" --policy --rollout 32 --steps 64 --warmup 32
          done ;;
-    pmcro) for c in FETCH_SIZE WRITE_SIZE; do
-            step "pmc_ro_W${a}_R${b}_$c" 120 rocprofv3 --pmc $c -d "$OUT/pmc_ro_W${a}_R${b}_$c" -o run --output-format csv \
-                -- $B --worlds "$a" --rollout "$b" --steps $((2 * b)) --warmup "$b"
+    pmcro) for ctr in FETCH_SIZE WRITE_SIZE; do
+            step "pmc_ro_W${a}_R${b}${sfx}_$ctr" 120 rocprofv3 --pmc $ctr -d "$OUT/pmc_ro_W${a}_R${b}${sfx}_$ctr" -o run \
+                --output-format csv -- $B --worlds "$a" --agents "$n" --rollout "$b" --steps $((2 * b)) --warmup "$b"
          done ;;
+    sqppo) step "sq_ppo_W$a" 120 rocprofv3 --pmc $SQ -d "$OUT/sq_ppo_W$a" -o run --output-format csv \
+            -- $B --worlds "$a" --policy --rollout 32 --steps 64 --warmup 32 ;;
     sq) step "sq_W${a}_N$b" 120 rocprofv3 --pmc $SQ -d "$OUT/sq_W${a}_N$b" -o run --output-format csv \
             -- $B --worlds "$a" --agents "$b" --steps 20 --warmup 5 ;;
     py) step "py_$(basename "$a" .py)${b:+_${b//[^A-Za-z0-9]/}}" 600 python3 "$R/$a" ${b//,/ } ;;

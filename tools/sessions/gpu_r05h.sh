@@ -9,7 +9,7 @@ cd "$R"
 OUT=gpurun_out/r05h
 mkdir -p $OUT
 export PYTHONUNBUFFERED=1
-for i in 1 2; do for v in prod ppsbar ppsflush; do
+for i in 1 2; do for v in prod ppsold ppsbar ppsflush; do
     if [ $v = prod ]; then lib=""; else lib=madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so; fi
     MADRONA_BB_LIB=$lib timeout -k 10 300 python3 tools/ppo_time.py --worlds 65536 --rollouts 4 2>&1 | grep -v amdgpu.ids \
         | grep -E "all records.*per_step=0" | sed "s|^|$v |" >> $OUT/pps_order_ab.txt || exit 1

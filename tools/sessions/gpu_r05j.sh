@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 5, session j: k_rollout_ppo (the fused PPO step's rollout in one
+# launch, no kernel boundary between steps) -- parity, A/B against one
+# k_step_ppo launch per step (MADRONA_BB_PPO_STEP_LOOP=0), trace; the 8 192-world
+# fused rollout with / without the two-lane row hand-off (xnosplit).
+set -u
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}
+cd "$R"
+OUT=gpurun_out/r05j
+mkdir -p $OUT
+export PYTHONUNBUFFERED=1
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu \
+    tests/test_ppo_step.py tests/test_policy_rollout.py > $OUT/pytest.log 2>&1
+rc=$?; tail -n 2 $OUT/pytest.log; [ $rc -eq 0 ] || exit $rc
+for i in 1 2; do for W in 65536 32768 131072; do for v in loop steps; do
+    if [ $v = loop ]; then L=1; else L=0; fi
+    MADRONA_BB_PPO_STEP_LOOP=$L timeout -k 10 300 python3 tools/ppo_time.py --worlds $W --rollouts 4 2>&1 | grep -v amdgpu.ids \
+        | grep -E "per_step=0" | sed "s|^|$v $W |" >> $OUT/pps_ab.txt || exit 1
+done; done; done
+for i in 1 2; do for v in prod xnosplit; do
+    if [ $v = prod ]; then lib=""; else lib=madrona_basketball_amd/_variants/$v/libmadrona_basketball_amd.so; fi
+    MADRONA_BB_LIB=$lib timeout -k 10 300 python3 tools/ppo_time.py --worlds 8192 --rollouts 6 2>&1 | grep -v amdgpu.ids \
+        | grep -E "all records.*per_step=0" | sed "s|^|$v 8192 |" >> $OUT/x_ab.txt || exit 1
+done; done
+timeout -k 10 400 python3 tools/ppo_step_trace.py --worlds 65536 > $OUT/pps_trace_W65536.txt 2>&1 || exit $?
+echo done

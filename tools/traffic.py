@@ -7,9 +7,11 @@ streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
 streaming stores.  Infinity-Cache hits are counted (not excluded).
 
 python tools/traffic.py <fetch_dir> <write_dir> <workload_key> [--out profiles/traffic.json]
-python tools/traffic.py <fetch_dir> <write_dir> W65536_PPO_R32 --ppo 2
-    (PPO rollout: every k_policy and k_step launch summed, per step = per
-    k_step launch x the parts a step is split into -- 2 from 32 768 worlds)
+python tools/traffic.py <fetch_dir> <write_dir> W65536_PPO_R32 --ppo 1
+    (PPO rollout: every k_policy, k_step and k_step_ppo launch summed, per
+    step = per step launch x the parts a step is split into -- 2 for the
+    two-stream split; the fused rollout: --ppo 1 --ppo-k 32, a
+    k_rollout_policy launch counting 32 steps)
 """
 import argparse
 import csv
@@ -30,17 +32,22 @@ def per_launch(d, counter, kernel_sub):
     return statistics.median(vals), len(vals)
 
 
-def ppo_per_step(d, counter, parts):
-    """Sum of counter over every k_policy / k_step launch, per PPO step."""
+def ppo_per_step(d, counter, parts, k_steps=1):
+    """Sum of counter over every k_policy / k_step / k_step_ppo /
+    k_rollout_policy launch, per PPO step (a k_rollout_policy launch is
+    k_steps steps)."""
     tot, steps, pol = 0.0, 0, 0.0
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
             k = r["Kernel_Name"]
-            if "k_step<" in k:
+            if "k_step<" in k or "k_step_ppo<" in k:
                 tot += float(r["Counter_Value"])
                 steps += 1
+            elif "k_rollout_policy<" in k:
+                tot += float(r["Counter_Value"])
+                steps += k_steps
             elif "k_policy" in k:
                 tot += float(r["Counter_Value"])
                 pol += float(r["Counter_Value"])
@@ -57,6 +64,7 @@ def main():
     ap.add_argument("key")
     ap.add_argument("--kernel", default="k_step<2, 0>")
     ap.add_argument("--ppo", type=int, default=0, help="PPO rollout mode: parts per step (1 or 2)")
+    ap.add_argument("--ppo-k", type=int, default=1, help="PPO rollout mode: steps per k_rollout_policy launch")
     ap.add_argument("--note", default="")
     ap.add_argument("--div", type=int, default=1, help="units (steps) per launch: the entry is per unit")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
@@ -67,14 +75,14 @@ def main():
     except (OSError, ValueError):
         data = {}
     if a.ppo:
-        fk, fpol, nf = ppo_per_step(a.fetch_dir, "FETCH_SIZE", a.ppo)
-        wk, wpol, nw = ppo_per_step(a.write_dir, "WRITE_SIZE", a.ppo)
+        fk, fpol, nf = ppo_per_step(a.fetch_dir, "FETCH_SIZE", a.ppo, a.ppo_k)
+        wk, wpol, nw = ppo_per_step(a.write_dir, "WRITE_SIZE", a.ppo, a.ppo_k)
         fetch, write = 2.0 * fk * 1024.0, wk * 1024.0
         pol = 2.0 * fpol * 1024.0 + wpol * 1024.0
         data[a.key] = {
             "bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
             "k_policy_bytes": pol, "k_step_bytes": fetch + write - pol,
-            "per": f"PPO step ({a.ppo} part(s): every k_policy and k_step launch of the run / (k_step launches / parts))",
+            "per": f"PPO step ({a.ppo} part(s): every policy / step / fused launch of the run / (steps / parts))",
             "k_step_launches": [nf, nw], "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> bytes",
             "source": a.note,
         }
