@@ -998,9 +998,6 @@ static int64_t ppo_fused_max_worlds()
     return v;
 }
 
-// PPO's loop as one k_step_ppo launch per step (the trainee's policy pass fused
-// behind the world step, its rows read from LDS) from this many worlds on;
-// MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never).
 // The fused step's rollout as one k_rollout_ppo launch (default) or as one
 // k_step_ppo launch per step (MADRONA_BB_PPO_STEP_LOOP=0; bit-identical).
 static bool ppo_step_loop()
@@ -1012,11 +1009,18 @@ static bool ppo_step_loop()
     return v;
 }
 
+// PPO's loop with the trainee's policy pass fused behind the world step (its
+// rows read from LDS; k_rollout_ppo) from this many worlds on, wherever the
+// register-resident k_rollout_policy (<= 16 384 worlds) is not taken:
+// measured 24 576 worlds 31.2 -> 20.0 us per step against the two-stream
+// split, while at 8 192 / 16 384 k_rollout_policy stays ahead (10.1 / 12.4 vs
+// 18.2 / 19.2; profiles/r05/k_small_ab.txt).
+// MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never).
 static int64_t ppo_step_fused_min_worlds()
 {
     static const int64_t v = [] {
         const char *e = std::getenv("MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS");
-        return (int64_t)(e && *e ? std::atoll(e) : 32768);
+        return (int64_t)(e && *e ? std::atoll(e) : 1);
     }();
     return v;
 }

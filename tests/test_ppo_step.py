@@ -1,5 +1,5 @@
 """k_rollout_ppo<2> / k_step_ppo<2>: PPO's rollout loop with the trainee's
-policy pass fused behind the world step (bb_rollout_policy from 32 768 worlds;
+policy pass fused behind the world step (bb_rollout_policy above 16 384 worlds;
 scripts/ppo.py:65-134 over scripts/env.py:126-170), the whole rollout in one
 launch (each wave steps its worlds K times; default) or one launch per step
 (MADRONA_BB_PPO_STEP_LOOP=0, child process).  Every recorded output
@@ -48,7 +48,8 @@ def fused_vs_per_step(W, n, trainee, stochastic, seed=7, step0=3, partial=False)
 @pytest.mark.gpu
 @pytest.mark.parametrize("W,n,trainee,stochastic", [(65536, 6, 0, True), (65536, 5, 1, False),
                                                     (65536, 32, 1, True), (32768, 8, 1, True),
-                                                    (40001, 4, 0, True), (131072, 3, 0, False)])
+                                                    (40001, 4, 0, True), (131072, 3, 0, False),
+                                                    (24576, 6, 1, True), (16385, 4, 0, False)])
 def test_gpu_fused_ppo_step_equals_per_step_launches(native_lib, W, n, trainee, stochastic):
     assert torch.cuda.is_available()
     b = fused_vs_per_step(W, n, trainee, stochastic)
