@@ -500,7 +500,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": ("bb::k_rollout<%d>" if (K and fused) else "bb::k_step<%d>") % args.agents,
+            "kernel": (("bb::k_rollout<%d>" if args.agents == 2 else "bb::k_rollout_shared<%d>") if (K and fused)
+                       else "bb::k_step<%d>") % args.agents,
             "kernel_avg_us": avg_kernel_s * 1e6,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },

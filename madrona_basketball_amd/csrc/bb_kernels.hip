@@ -362,11 +362,14 @@ __device__ __forceinline__ void row_store(char *base, uint32_t off, vf4 v)
 
 // The record of agent `agent`'s rows (Params::rec_obs, N = 2): row r of the
 // wave's tile (world r / N, agent r % N) also goes to base + (r / N) * 512
-// (+ the pass's piece offset); base == nullptr: no record.
+// (+ the pass's piece offset); base == nullptr: no record.  mirror: every
+// row also to base at its own offset (a K-step rollout's last step: the rows
+// into the sim's observation tensor as well as the recorded buffer).
 struct RecRows {
     char *base;
     int agent;
     bool only;  // the agent's rows into the record only (Params::rec_only)
+    bool mirror = false;
 };
 #ifndef BB_REC_AUX
 #define BB_REC_AUX 2  // record rows: non-temporal (a fresh [K][W][128] buffer, beyond the cache for K >= 8)
@@ -390,9 +393,9 @@ __device__ __forceinline__ void flush_rows(const float *tile, char *base, uint64
             if (b0 + j < QT) {
                 ok[j] = (QN == QT || q < QN) && (ALL || ((staged >> r) & 1ull));
                 go[j] = (uint32_t)(r * (RSTR * OW * 4) + q * 16);
-                rk[j] = ok[j] && (r % N) == rec.agent;
+                rk[j] = ok[j] && (rec.mirror || (r % N) == rec.agent);
                 sk[j] = ok[j] && !(rec.only && (r % N) == rec.agent);
-                ro[j] = (uint32_t)((r / N) * (OW * 4) + q * 16);
+                ro[j] = rec.mirror ? go[j] : (uint32_t)((r / N) * (OW * 4) + q * 16);
                 if (ok[j]) {
                     v[j] = *(const vf4 *)(tile + r * RS + 4 * q);
                     if (QZ < QN && q >= QZ) v[j] = vf4{0.f, 0.f, 0.f, 0.f};
@@ -523,9 +526,12 @@ __device__ __forceinline__ void lane_shared_obs(const World<N> &v, const Ctx &c,
     }
 }
 
+// mirror_sim (wave-uniform; not with REC): every row also into the sim's own
+// observation tensor (c.p->c.obs), obs being a recorded buffer.
 template <int N, int MODE, class T = PhasedTile<N>, bool REC = false>
 __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k,
-                                               int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs)
+                                               int lane, int64_t w0, int64_t w, bool active, float *tile, float *obs,
+                                               bool mirror_sim = false)
 {
     constexpr int OW = obs_width(N);
     SharedObs<N> sh;
@@ -549,9 +555,12 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
         RecRows rec{nullptr, 0, false};
         if constexpr (REC)
             rec = RecRows{(char *)(c.p->rec_obs + w0 * (int64_t)OW), c.p->rec_agent, c.p->rec_only != 0};
+        else if (mirror_sim)
+            rec = RecRows{(char *)(c.p->c.obs + w0 * N * (int64_t)OW), 0, false, true};
         if (active && !fast) {
             if (!(rec.base && rec.only && k == rec.agent)) fill_obs_slow(v, c, 0, grow, ib);
-            if (rec.base && k == rec.agent) fill_obs_slow(v, c, 0, c.p->rec_obs + w * (int64_t)OW, ib);
+            if (REC && rec.base && k == rec.agent) fill_obs_slow(v, c, 0, c.p->rec_obs + w * (int64_t)OW, ib);
+            if (!REC && mirror_sim) fill_obs_slow(v, c, 0, c.p->c.obs + (w * N + k) * (int64_t)OW, ib);
         }
         obs_phases<N, MODE, T>(v, c, sh, share, fast, tile, obs, w0 * N, lane, ib, rec);
         if (REC && T::QW < OW / 4) {
@@ -631,20 +640,27 @@ __device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
 
 // Pass PHASE of the observation rows of a wave that only writes rows (the
 // observation wave of k_rollout_split): its own tile, wave-local ordering.
+// mirror (wave-uniform, optional): every row also into this [W][N][OBSW] base.
 template <int N, int PHASE, class T = StepTile<N, false>>
 __device__ __forceinline__ void obs_pass_wave(const World<N> &v, const Ctx &c, int32_t ib, bool share, int k, int lane,
-                                              int64_t w0, int64_t w, bool active, float *tile, float *obs)
+                                              int64_t w0, int64_t w, bool active, float *tile, float *obs,
+                                              float *mirror = nullptr)
 {
+    constexpr int OW = obs_width(N);
     SharedObs<N> sh;
     lane_shared_obs(v, c, active, sh);
     const bool fast = active && canonical_slots(v, 0);
     // rows the tile does not carry are written whole by the first pass's wave
-    if (PHASE == 0 && active && !fast) fill_obs_slow(v, c, 0, obs + (w * N + k) * (int64_t)obs_width(N), ib);
+    if (PHASE == 0 && active && !fast) {
+        fill_obs_slow(v, c, 0, obs + (w * N + k) * (int64_t)OW, ib);
+        if (mirror) fill_obs_slow(v, c, 0, mirror + (w * N + k) * (int64_t)OW, ib);
+    }
     if (fast) emit_phase<N, T, PHASE>(v, c, sh, share, tile + lane * T::RS, ib);
     wave_sync();
     constexpr int Q0 = PHASE * T::QP, QN = (T::QW - Q0 < T::QP) ? T::QW - Q0 : T::QP;
     constexpr int QZ = T::QU - Q0 < 0 ? 0 : (T::QU - Q0 < QN ? T::QU - Q0 : QN);
-    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, w0 * N, __ballot(fast), lane);
+    const RecRows rec{mirror ? (char *)(mirror + w0 * N * (int64_t)OW) : nullptr, 0, false, true};
+    flush_tile<N, T::QP, T::RS, Q0, QN, 1, QZ, T::AUX>(tile, obs, w0 * N, __ballot(fast), lane, rec);
 }
 
 // ------------------------------------------------------------------ rollout
@@ -748,8 +764,10 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
         }
         __syncthreads();  // parked rows read before the tile is rewritten
 #if !defined(BB_RO_NO_OBS)
+        // (the last step of a recorded rollout: the rows into the sim's tensor too)
         agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane_t, w0, w_t, active, tile,
-                                        r.obs + (int64_t)t * r.obs_step);
+                                        r.obs + (int64_t)t * r.obs_step,
+                                        BB_ROLLOUT_MIRROR && t + 1 == r.steps && r.obs_step != 0);
 #endif
         __syncthreads();  // the tile is rewritten by the next step
     }
@@ -898,10 +916,12 @@ __device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArg
         const bool share = u[SplitView<N>::WORDS - 1] != 0u;
         const Ctx c = make_ctx(p, w, k == 0);
         float *obs = r.obs + (int64_t)t * r.obs_step;
-        obs_pass_wave<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+        // the last step of a recorded rollout: the rows into the sim's tensor too
+        float *mirror = (BB_ROLLOUT_MIRROR && t + 1 == r.steps && r.obs_step != 0) ? p.c.obs : nullptr;
+        obs_pass_wave<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs, mirror);
         wave_sync();  // the tile is rewritten by the next pass
         if constexpr (T::PH > 1) {
-            obs_pass_wave<N, 1, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs);
+            obs_pass_wave<N, 1, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs, mirror);
             wave_sync();
         }
         static_assert(T::PH <= 2, "two row passes");
@@ -1291,7 +1311,7 @@ __global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), MINW) void k_rollout_polic
 
 // ------------------------------------------------------------------ PPO step
 // k_step_ppo<2>: one step of PPO's rollout loop with the trainee's policy pass
-// fused behind it (bb_rollout_policy from 32 768 worlds; scripts/ppo.py:65-134
+// fused behind it (bb_rollout_policy above 16 384 worlds; scripts/ppo.py:65-134
 // over scripts/env.py:126-170).  A wave steps its 32 worlds exactly as
 // k_step<2> does (agent lanes, the world in registers), then the policy of
 // step k + 1 runs on the trainee's rows while they are in LDS: no second

@@ -21,6 +21,12 @@ enum StepMode : int {
 
 // K-step rollout (bb_rollout): step t reads actions + t*W*N*6 and writes its
 // observation rows, rewards and done flags at obs/reward/done + t*(row stride).
+// The N = 2 K-step rollout kernels store the last step's rows into the sim's
+// observation tensor as well as the recorded buffer (instead of a copy after
+// the launch; 0: the copy, timing A/B).
+#ifndef BB_ROLLOUT_MIRROR
+#define BB_ROLLOUT_MIRROR 1
+#endif
 struct RolloutArgs {
     int32_t *actions;  // [K][W][N][6]   (defence overrides written back)
     float *obs;        // [K][W][N][OBSW]
@@ -46,7 +52,7 @@ struct PolicyRolloutArgs {
 };
 
 // One step of PPO's rollout loop with the policy fused behind it
-// (k_step_ppo<2>, bb_rollout_policy from 32 768 worlds): step k on the
+// (k_step_ppo<2> / k_rollout_ppo<2>, bb_rollout_policy above 16 384 worlds): step k on the
 // trainee's actions already in the sim's action column, then the policy on the
 // trainee's rows after the step (scripts/ppo.py:65-134 over env.py:126-170) --
 // the actions of step k + 1 into the action column, buffer.obs/actions/

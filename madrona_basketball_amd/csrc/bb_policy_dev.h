@@ -18,6 +18,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "bb_policy.h"
+#include <type_traits>
 
 namespace bb {
 
@@ -128,6 +129,20 @@ __device__ __forceinline__ void ln_relu_to_tile(f32x4 a0, f32x4 a1, float bias0,
 // operations on the same inputs), so rows are bit-identical to MT = 4's.
 // (Until round 5 the maxima and the exp terms were separate phases with an
 // LDS round trip between them: 8 192-world PPO trace 0.64 + 0.48 + 0.84 us.)
+// The largest bucket among round j's (buckets p + lpr j, p < lpr).
+__host__ __device__ constexpr int bucket_round_max(int lpr, int j)
+{
+    int m = 0;
+    for (int p = 0; p < lpr; p++) {
+        const int b = p + lpr * j;
+        if (b < POL_BUCKETS && pol_bucket(b) > m) m = pol_bucket(b);
+    }
+    return m;
+}
+static_assert(bucket_round_max(2, 0) == 8 && bucket_round_max(2, 1) == 3 && bucket_round_max(2, 2) == 2 &&
+                  bucket_round_max(4, 1) == 2 && bucket_round_max(8, 0) == 8,
+              "bucket rounds");
+
 // The bucket pass's LDS exchange of one wave (R rows).
 template <int R>
 struct BucketLds {
@@ -230,53 +245,61 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     // draw over the terms in logit order), logit[a] - (max + log(sum)) --
     // pol_bucket_term's operations, the terms never leave the registers
     bucket_stamp(ts, 0, lane);
+    // round j: every lane's bucket part + LPR j; the loops run to the largest
+    // bucket of the round (compile time: 8, then 3 and 2 at LPR 2), not to 8
+    const auto round = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < BPL) {
+            constexpr int NBM = bucket_round_max(LPR, j);
+            const int b = part + LPR * j;
+            if (b < POL_BUCKETS) {
+                const int o = pol_bucket_off(b), nb = pol_bucket(b);
+                float l[NBM];
 #pragma unroll
-    for (int j = 0; j < BPL; j++) {
-        const int b = part + LPR * j;
-        if (b < POL_BUCKETS) {
-            const int o = pol_bucket_off(b), nb = pol_bucket(b);
-            float l[8];
+                for (int i = 0; i < NBM; i++) l[i] = i < nb ? lg[o + i] : 0.f;
+                float mx = l[0];
 #pragma unroll
-            for (int i = 0; i < 8; i++) l[i] = i < nb ? lg[o + i] : 0.f;
-            float mx = l[0];
+                for (int i = 1; i < NBM; i++)
+                    if (i < nb) mx = l[i] > mx ? l[i] : mx;
+                float e[NBM];
 #pragma unroll
-            for (int i = 1; i < 8; i++)
-                if (i < nb) mx = l[i] > mx ? l[i] : mx;
-            float e[8];
+                for (int i = 0; i < NBM; i++) e[i] = pol_expf(l[i] - mx);
+                float sum = e[0];
 #pragma unroll
-            for (int i = 0; i < 8; i++) e[i] = pol_expf(l[i] - mx);
-            float sum = e[0];
+                for (int i = 1; i < NBM; i++)
+                    if (i < nb) sum = sum + e[i];
+                int act = 0;
+                if (stochastic) {
+                    const float u = PRE ? pre->u[j] : own.u[j];
+                    const float t = u * sum;
+                    float cs = 0.f;
+                    act = nb - 1;
 #pragma unroll
-            for (int i = 1; i < 8; i++)
-                if (i < nb) sum = sum + e[i];
-            int act = 0;
-            if (stochastic) {
-                const float u = PRE ? pre->u[j] : own.u[j];
-                const float t = u * sum;
-                float cs = 0.f;
-                act = nb - 1;
+                    for (int i = 0; i < NBM - 1; i++) {
+                        if (i < nb - 1) {
+                            cs = cs + e[i];
+                            if (act == nb - 1 && cs > t) act = i;
+                        }
+                    }
+                } else {
+                    float best = l[0];
 #pragma unroll
-                for (int i = 0; i < 7; i++) {
-                    if (i < nb - 1) {
-                        cs = cs + e[i];
-                        if (act == nb - 1 && cs > t) act = i;
+                    for (int i = 1; i < NBM; i++) {
+                        if (i < nb && l[i] > best) { best = l[i]; act = i; }  // first maximum
                     }
                 }
-            } else {
-                float best = l[0];
+                const float lse = mx + pol_logf(sum);
+                float la = l[0];
 #pragma unroll
-                for (int i = 1; i < 8; i++) {
-                    if (i < nb && l[i] > best) { best = l[i]; act = i; }  // first maximum
-                }
+                for (int i = 1; i < NBM; i++) la = act == i ? l[i] : la;
+                abuf[r][b] = act;
+                tbuf[r][b] = la - lse;
             }
-            const float lse = mx + pol_logf(sum);
-            float la = l[0];
-#pragma unroll
-            for (int i = 1; i < 8; i++) la = act == i ? l[i] : la;
-            abuf[r][b] = act;
-            tbuf[r][b] = la - lse;
         }
-    }
+    };
+    round(std::integral_constant<int, 0>());
+    round(std::integral_constant<int, 1>());
+    round(std::integral_constant<int, 2>());
     pol_wave_sync();
     bucket_stamp(ts, 1, lane);
     bucket_stamp(ts, 2, lane);
