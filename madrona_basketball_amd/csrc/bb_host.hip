@@ -816,9 +816,9 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
             if (e != hipSuccess) return hip_fail(e, "copy last reward/done");
         }
     }
-    // the written part of every row (the zero tail stays); the N = 2 rollout
-    // kernels store the last step's rows into the sim's tensor themselves
-    if (obs_out && !(BB_ROLLOUT_MIRROR && fused && s->n == 2)) {
+    // the written part of every row (the zero tail stays); the rollout kernels
+    // store the last step's rows into the sim's tensor themselves
+    if (obs_out && !fused) {
         hipError_t e = hipMemcpy2DAsync(s->p.c.obs, (size_t)ow * 4, last_obs, (size_t)ow * 4, (size_t)used_bytes,
                                         (size_t)rows, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_fail(e, "copy last observations");

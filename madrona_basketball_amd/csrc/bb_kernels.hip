@@ -767,7 +767,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
         // (the last step of a recorded rollout: the rows into the sim's tensor too)
         agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane_t, w0, w_t, active, tile,
                                         r.obs + (int64_t)t * r.obs_step,
-                                        BB_ROLLOUT_MIRROR && t + 1 == r.steps && r.obs_step != 0);
+                                        t + 1 == r.steps && r.obs_step != 0);
 #endif
         __syncthreads();  // the tile is rewritten by the next step
     }
@@ -917,7 +917,7 @@ __device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArg
         const Ctx c = make_ctx(p, w, k == 0);
         float *obs = r.obs + (int64_t)t * r.obs_step;
         // the last step of a recorded rollout: the rows into the sim's tensor too
-        float *mirror = (BB_ROLLOUT_MIRROR && t + 1 == r.steps && r.obs_step != 0) ? p.c.obs : nullptr;
+        float *mirror = (t + 1 == r.steps && r.obs_step != 0) ? p.c.obs : nullptr;
         obs_pass_wave<N, 0, T>(v, c, ib, share, k, lane_t, w0, w, active, tile, obs, mirror);
         wave_sync();  // the tile is rewritten by the next pass
         if constexpr (T::PH > 1) {
@@ -2304,12 +2304,19 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
         const int32_t ib = inbounder_id(s);
         const bool share = obs_sharable(s);
         LaneSources<N> src;
+        // the last step of a recorded rollout: the rows into the sim's tensor too
+        const bool mirror = t + 1 == r.steps && r.obs_step != 0;
         if (active) {
             src.compute(s, c, k_t, ib, share);
             if (!share) {  // rows the pieces do not cover: straight from the lane
                 float *grow = obs_t + row * (int64_t)OW;
                 if (canonical_slots(s, k_t)) fill_obs_fast(s, c, k_t, grow, ib);
                 else fill_obs_slow(s, c, k_t, grow, ib);
+                if (mirror) {
+                    float *srow = p.c.obs + row * (int64_t)OW;
+                    if (canonical_slots(s, k_t)) fill_obs_fast(s, c, k_t, srow, ib);
+                    else fill_obs_slow(s, c, k_t, srow, ib);
+                }
             }
         }
         const uint64_t rows = __ballot(active && share);
@@ -2326,6 +2333,7 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
             }
         }
         obs_parts<N, AUX, 0, SM>(sm, src, rows, teams, obs_t, w0 * N, lane_t, slot, k_t, active, share);
+        if (mirror) obs_parts<N, AUX, 0, SM>(sm, src, rows, teams, p.c.obs, w0 * N, lane_t, slot, k_t, active, share);
         __syncthreads();  // the table's readers are done
         if constexpr (SR::KEEP) {
             if (lane_used) {
