@@ -243,8 +243,9 @@ int bb_policy_forward(const bb_policy_weights *w, int32_t exec_mode, int32_t gpu
  * the opponent samples with seed ^ 0x9E3779B9.  Equal, bit for bit, to n x
  * (bb_policy_forward on the trainee rows; bb_step) with the reads above.
  * On gfx950 without an opponent, up to 16 384 worlds one fused launch runs
- * all n steps (BB_PPO_PATH_FUSED_ROLLOUT); from 32 768 worlds a policy launch
- * and then one launch per step that runs the step and the next policy pass
+ * all n steps with the worlds in registers (BB_PPO_PATH_FUSED_ROLLOUT); above,
+ * a policy launch and then one launch in which every wave runs its worlds' n
+ * steps, each followed by the next policy pass on the rows in LDS
  * (BB_PPO_PATH_FUSED_STEP).  flags BB_ROLLOUT_PER_STEP forces a policy launch
  * and a step launch per step instead (so does an opponent); from 32 768
  * worlds those per-step launches of two world halves go to `stream` and to a
@@ -266,7 +267,7 @@ int bb_rollout_policy(bb_sim *sim, const bb_policy_weights *w, const bb_policy_w
  * bytes that path must move: HBM roofline of the PPO loop). */
 #define BB_PPO_PATH_HOST 0          /* CPU mode: the host executor */
 #define BB_PPO_PATH_FUSED_ROLLOUT 1 /* one k_rollout_policy launch for all n steps */
-#define BB_PPO_PATH_FUSED_STEP 2    /* a policy launch, then one k_step_ppo per step */
+#define BB_PPO_PATH_FUSED_STEP 2    /* a policy launch, then k_rollout_ppo (step + next policy pass, n times) */
 #define BB_PPO_PATH_PER_STEP 3      /* a policy launch and a step launch per step */
 int32_t bb_rollout_policy_path(const bb_sim *sim, int32_t with_opponent, uint32_t flags);
 int64_t bb_rollout_policy_bytes(const bb_sim *sim, int32_t with_opponent, uint32_t flags, int32_t n);

@@ -1168,10 +1168,18 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         const int64_t waves = (W + 31) / 32;
         uint64_t *ts = nullptr;
         if (trace && *trace && hipMalloc(&ts, (size_t)n * waves * bb::PPS_TRACE_POINTS * 8) != hipSuccess) ts = nullptr;
-        hipError_t e = bb::launch_policy(pass(0, false), st);
+        // (the k_step_ppo launches need the policy pass of step 0 before them;
+        // k_rollout_ppo runs it itself)
+        hipError_t e = ppo_step_loop() ? hipSuccess : bb::launch_policy(pass(0, false), st);
         if (e == hipSuccess && ppo_step_loop()) {
             // the whole rollout in one k_rollout_ppo launch
             bb::PpoStepArgs a{};
+            a.pass0 = 1;
+            a.step0 = step0;
+            a.obs0 = out->obs;
+            a.act0 = out->actions;
+            a.log_prob0 = out->log_prob;
+            a.value0 = out->value;
             a.diag = diag;
             a.diag_ts = ts;
             a.w = policy_weights(w);

@@ -65,6 +65,14 @@ struct PpoStepArgs {
     int32_t last;               // the rollout's last step: every row into the sim's obs, value only
     uint32_t seed, step;        // the policy's sampling key (seed, step0 + k + 1)
     float *value_last;          // k_rollout_ppo: next_value (the value output of its last step)
+    // k_rollout_ppo: the policy pass of step 0 in the launch (on the sim's rows
+    // of the trainee before the first step, key step0): buffer.obs / actions /
+    // log_probs / values[0] (each optional); pass0 = 0: done by a launch before
+    int32_t pass0;
+    uint32_t step0;
+    float *obs0;
+    int32_t *act0;
+    float *log_prob0, *value0;
     // diagnostics only (timing attribution; the outputs are then wrong):
     // diag bit 0 no bucket pass, 1 no LayerNorm-1 / layer 2 / heads, 2 no
     // layer-1 MFMAs, 3 no buffer.obs stores; diag_ts: PPS_TRACE_POINTS clocks

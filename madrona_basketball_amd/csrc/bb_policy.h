@@ -69,13 +69,18 @@ constexpr int POL_TRACE_POINTS = 8;
 // the host's fmaf), half the instructions of the separately rounded mul + add
 // chains (the translation units build with -ffp-contract=off) -- the bucket
 // pass evaluates 19 of these per row (round 5).
+//
+// Branch-free: the special cases (NaN, overflow, underflow; log of 0, inf or
+// a negative) are selected at the end, the polynomial path runs on an input
+// clamped into its range -- equal to the input wherever that path's result is
+// the one returned, so every value is the same as with early returns.  (With
+// early returns each call was three nested exec-mask branches on the device,
+// and the bucket pass's 8 exps of a bucket ran one after another.)
 BB_HD float pol_expf(float x)
 {
-    if (x != x) return x;
-    if (x > 88.7f) return __builtin_inff();
-    if (x < -103.9f) return 0.f;
-    const float k = __builtin_rintf(x * 1.44269504f);
-    float r = __builtin_fmaf(-k, 0.693145752f, x);    // ln2 high part
+    const float xc = __builtin_fminf(__builtin_fmaxf(x, -104.0f), 89.0f);  // (NaN -> -104)
+    const float k = __builtin_rintf(xc * 1.44269504f);
+    float r = __builtin_fmaf(-k, 0.693145752f, xc);   // ln2 high part
     r = __builtin_fmaf(-k, 1.42860677e-06f, r);        // ln2 low part
     float p = 1.0f / 5040.0f;                          // Taylor to r^7 on |r| <= 0.347
     p = __builtin_fmaf(p, r, 1.0f / 720.0f);
@@ -85,16 +90,21 @@ BB_HD float pol_expf(float x)
     p = __builtin_fmaf(p, r, 0.5f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
-    return __builtin_ldexpf(p, (int)k);
+    float y = __builtin_ldexpf(p, (int)k);
+    y = x < -103.9f ? 0.f : y;
+    y = x > 88.7f ? __builtin_inff() : y;
+    return x != x ? x : y;
 }
 BB_HD float pol_logf(float x)
 {
-    if (x != x || x < 0.f) return __builtin_nanf("");
-    if (x == 0.f) return -__builtin_inff();
-    if (x == __builtin_inff()) return x;
+    // the polynomial path on a finite positive stand-in where x is special
+    const bool special = !(x > 0.f) || x == __builtin_inff();  // NaN, <= 0, inf
+    const float xs = special ? 1.0f : x;
     int e = 0;
-    float m = __builtin_frexpf(x, &e);       // [0.5, 1)
-    if (m < 0.707106781f) { m = m * 2.0f; e -= 1; }
+    float m = __builtin_frexpf(xs, &e);      // [0.5, 1)
+    const bool lo = m < 0.707106781f;
+    m = lo ? m * 2.0f : m;
+    e = lo ? e - 1 : e;
     const float s = (m - 1.0f) / (m + 1.0f);  // |s| <= 0.1716
     const float z = s * s;
     float p = 1.0f / 11.0f;
@@ -104,7 +114,9 @@ BB_HD float pol_logf(float x)
     p = __builtin_fmaf(p, z, 1.0f / 3.0f);
     const float lm = 2.0f * __builtin_fmaf(s * z, p, s);
     const float k = (float)e;
-    return __builtin_fmaf(k, 0.693145752f, __builtin_fmaf(k, 1.42860677e-06f, lm));
+    const float y = __builtin_fmaf(k, 0.693145752f, __builtin_fmaf(k, 1.42860677e-06f, lm));
+    if (!special) return y;
+    return x == 0.f ? -__builtin_inff() : (x == __builtin_inff() ? x : __builtin_nanf(""));
 }
 BB_HD float pol_clamp(float x) { return __builtin_fminf(__builtin_fmaxf(x, -5.f), 5.f); }  // v_max / v_min
 BB_HD float pol_relu(float x) { return x > 0.f ? x : 0.f; }
@@ -130,11 +142,11 @@ BB_HD int pol_inverse_cdf(const float (&e)[NB], int nb, float s, float u)
     float c = 0.f;
     int a = nb - 1;
 #pragma unroll
-    for (int i = 0; i < NB; i++) {
-        if (i < nb - 1) {
-            c = c + e[i];
-            if (a == nb - 1 && c > t) a = i;
-        }
+    for (int i = 0; i < NB; i++) {  // (selects, no branches)
+        const bool in = i < nb - 1;
+        const float ci = c + e[i];
+        a = (in && a == nb - 1 && ci > t) ? i : a;
+        c = in ? ci : c;
     }
     return a;
 }

@@ -256,7 +256,10 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
                 const int o = pol_bucket_off(b), nb = pol_bucket(b);
                 float l[NBM];
 #pragma unroll
-                for (int i = 0; i < NBM; i++) l[i] = i < nb ? lg[o + i] : 0.f;
+                for (int i = 0; i < NBM; i++) {  // (in the row: o + NBM <= 21 of its 33 floats)
+                    const float li = lg[o + i];
+                    l[i] = i < nb ? li : 0.f;
+                }
                 float mx = l[0];
 #pragma unroll
                 for (int i = 1; i < NBM; i++)
@@ -275,17 +278,19 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
                     float cs = 0.f;
                     act = nb - 1;
 #pragma unroll
-                    for (int i = 0; i < NBM - 1; i++) {
-                        if (i < nb - 1) {
-                            cs = cs + e[i];
-                            if (act == nb - 1 && cs > t) act = i;
-                        }
+                    for (int i = 0; i < NBM - 1; i++) {  // (selects, no branches)
+                        const bool in = i < nb - 1;
+                        const float ci = cs + e[i];
+                        act = (in && act == nb - 1 && ci > t) ? i : act;
+                        cs = in ? ci : cs;
                     }
                 } else {
                     float best = l[0];
 #pragma unroll
-                    for (int i = 1; i < NBM; i++) {
-                        if (i < nb && l[i] > best) { best = l[i]; act = i; }  // first maximum
+                    for (int i = 1; i < NBM; i++) {  // first maximum
+                        const bool up = i < nb && l[i] > best;
+                        best = up ? l[i] : best;
+                        act = up ? i : act;
                     }
                 }
                 const float lse = mx + pol_logf(sum);
