@@ -364,7 +364,9 @@ def main():
             barrier()
             fused2 = bool(L0.bb_rollout_fused(n2)) and K2 > 0
             if fused2:
-                b2 = W2 * (K2 * L0.bb_rollout_bytes_per_world_step(n2) + L0.bb_rollout_state_bytes_per_world(n2))
+                # + at N = 2 the last step's rows into the sim's own tensor (recorded)
+                b2 = W2 * (K2 * L0.bb_rollout_bytes_per_world_step(n2) + L0.bb_rollout_state_bytes_per_world(n2)
+                           + (L0.bb_rollout_bytes_per_world_step(n2) - 32 * n2 if n2 == 2 else 0))
             else:
                 b2 = L0.bb_algorithmic_bytes_per_world(n2) * W2 * (K2 or 1)
             key = f"W{W2}_N{n2}" + (f"_R{K2}" if K2 else "")
@@ -451,9 +453,12 @@ def main():
     L = _lib.load()
     if K and fused:
         # per launch: the state once in and out, and per step only the action
-        # rows in and the recorded rows (obs, reward, done) out
+        # rows in and the recorded rows (obs, reward, done) out;
+        # recorded, the last step's rows also into the sim's own tensor
+        mirror = (0 if args.no_record or args.agents != 2
+                  else L.bb_rollout_bytes_per_world_step(args.agents) - 32 * args.agents)
         bytes_per_launch = W * (K * L.bb_rollout_bytes_per_world_step(args.agents)
-                                + L.bb_rollout_state_bytes_per_world(args.agents))
+                                + L.bb_rollout_state_bytes_per_world(args.agents) + mirror)
     else:
         bytes_per_launch = L.bb_algorithmic_bytes_per_world(args.agents) * W
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9

@@ -816,9 +816,11 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
             if (e != hipSuccess) return hip_fail(e, "copy last reward/done");
         }
     }
-    // the written part of every row (the zero tail stays); the rollout kernels
-    // store the last step's rows into the sim's tensor themselves
-    if (obs_out && !fused) {
+    // the written part of every row (the zero tail stays); the N = 2 rollout
+    // kernels store the last step's rows into the sim's tensor themselves (at
+    // N >= 4 that second store made every step of k_rollout_shared slower:
+    // 1 470 -> 1 677 us per 32-step launch, against a copy of ~200 us)
+    if (obs_out && !(fused && s->n == 2)) {
         hipError_t e = hipMemcpy2DAsync(s->p.c.obs, (size_t)ow * 4, last_obs, (size_t)ow * 4, (size_t)used_bytes,
                                         (size_t)rows, hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_fail(e, "copy last observations");
@@ -1170,11 +1172,12 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         if (trace && *trace && hipMalloc(&ts, (size_t)n * waves * bb::PPS_TRACE_POINTS * 8) != hipSuccess) ts = nullptr;
         // (the k_step_ppo launches need the policy pass of step 0 before them;
         // k_rollout_ppo runs it itself)
-        hipError_t e = ppo_step_loop() ? hipSuccess : bb::launch_policy(pass(0, false), st);
+        const bool in_kernel = ppo_step_loop();
+        hipError_t e = in_kernel ? hipSuccess : bb::launch_policy(pass(0, false), st);
         if (e == hipSuccess && ppo_step_loop()) {
             // the whole rollout in one k_rollout_ppo launch
             bb::PpoStepArgs a{};
-            a.pass0 = 1;
+            a.pass0 = in_kernel ? 1 : 0;
             a.step0 = step0;
             a.obs0 = out->obs;
             a.act0 = out->actions;

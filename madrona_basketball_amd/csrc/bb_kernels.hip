@@ -2041,7 +2041,7 @@ __device__ __forceinline__ void read_batch(const float *e, const int (&src)[NP][
 template <int N, int AUX, int S0, int S1, int NP, int RB, int A0, class SM>
 __device__ __forceinline__ void emit_slot_batches(const SM &sm, const int (&src)[NP][N][4],
                                                   const int (&dtm)[NP][4], uint64_t rows, uint64_t teams, char *base,
-                                                  char *mbase, int lane, int slot, vf4 (&cur)[RB][NP])
+                                                  int lane, int slot, vf4 (&cur)[RB][NP])
 {
     constexpr int QR = ObsSrc<N>::QR;
     vf4 nxt[RB][NP];
@@ -2057,21 +2057,17 @@ __device__ __forceinline__ void emit_slot_batches(const SM &sm, const int (&src)
 #pragma unroll
         for (int p = 0; p < NP; p++)
             if (p * WAVE + lane < QR) row_store<AUX>(base, ((uint32_t)r * QR + p * WAVE + lane) * 16u, cur[b][p]);
-        if (mbase)  // (wave-uniform) the mirror: the same rows at the same offsets
-#pragma unroll
-            for (int p = 0; p < NP; p++)
-                if (p * WAVE + lane < QR) row_store<AUX>(mbase, ((uint32_t)r * QR + p * WAVE + lane) * 16u, cur[b][p]);
     }
 #pragma unroll
     for (int b = 0; b < RB; b++)
 #pragma unroll
         for (int p = 0; p < NP; p++) cur[b][p] = nxt[b][p];
     if constexpr (A0 + RB < N)
-        emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB, SM>(sm, src, dtm, rows, teams, base, mbase, lane, slot, cur);
+        emit_slot_batches<N, AUX, S0, S1, NP, RB, A0 + RB, SM>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
 template <int N, int AUX, int S0, int S1, class SM>
 __device__ __forceinline__ void emit_pieces_rows(const SM &sm, uint64_t rows, uint64_t teams, float *obs,
-                                                 int64_t row0, int lane, float *mobs = nullptr)
+                                                 int64_t row0, int lane)
 {
     using S = ObsSrc<N>;
     constexpr int WPW = SM::WPW, QR = S::QR, NP = (QR + WAVE - 1) / WAVE;
@@ -2091,38 +2087,34 @@ __device__ __forceinline__ void emit_pieces_rows(const SM &sm, uint64_t rows, ui
         }
     }
     char *base = (char *)(obs + row0 * obs_width(N));  // wave-uniform
-    char *mbase = mobs ? (char *)(mobs + row0 * obs_width(N)) : nullptr;
     static_assert(S1 <= WPW && S1 - S0 <= SM::SPP, "part of the source table");
     vf4 cur[RB][NP];
     read_batch<N, NP, RB, 0>(sm.e[0], src, dtm, teams >> (S0 * N), cur);
     for (int slot = S0; slot < S1; slot++)
-        emit_slot_batches<N, AUX, S0, S1, NP, RB, 0, SM>(sm, src, dtm, rows, teams, base, mbase, lane, slot, cur);
+        emit_slot_batches<N, AUX, S0, S1, NP, RB, 0, SM>(sm, src, dtm, rows, teams, base, lane, slot, cur);
 }
 
 template <int N, int AUX, int S0, int S1, class SM>
 __device__ __forceinline__ void emit_pieces(const SM &sm, uint64_t rows, uint64_t teams, float *obs,
-                                            int64_t row0, int lane, float *mobs = nullptr)
+                                            int64_t row0, int lane)
 {
-    emit_pieces_rows<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane, mobs);
+    emit_pieces_rows<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane);
 }
 
 // The source table written and emitted part by part (BB_OBS_PARTS): the
 // world state is dead once every lane holds its sources; each part's lanes
 // put theirs, the wave emits that part's rows, and the next part overlays it.
 template <int N, int AUX, int P = 0, class SM = SharedLds<N>>
-// mobs (wave-uniform, optional): every row also into this [W][N][OBSW] base.
 __device__ __forceinline__ void obs_parts(SM &sm, const LaneSources<N> &src, uint64_t rows, uint64_t teams, float *obs,
-                                          int64_t row0, int lane, int slot, int k, bool active, bool share,
-                                          float *mobs = nullptr)
+                                          int64_t row0, int lane, int slot, int k, bool active, bool share)
 {
     using SL = SM;
     constexpr int S0 = P * SL::SPP, S1 = (S0 + SL::SPP < SL::WPW) ? S0 + SL::SPP : SL::WPW;
     __syncthreads();  // the world state (or the previous part) is dead: this part overlays it
     if (active && slot >= S0 && slot < S1) src.put(sm.e[slot - S0], k, share);
     __syncthreads();
-    emit_pieces<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane, mobs);
-    if constexpr (P + 1 < SL::PARTS)
-        obs_parts<N, AUX, P + 1, SM>(sm, src, rows, teams, obs, row0, lane, slot, k, active, share, mobs);
+    emit_pieces<N, AUX, S0, S1, SM>(sm, rows, teams, obs, row0, lane);
+    if constexpr (P + 1 < SL::PARTS) obs_parts<N, AUX, P + 1, SM>(sm, src, rows, teams, obs, row0, lane, slot, k, active, share);
 }
 
 template <int N, int MODE, int PHASE = 0>
@@ -2393,19 +2385,12 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
         const int32_t ib = inbounder_id(s);
         const bool share = obs_sharable(s);
         LaneSources<N> src;
-        // the last step of a recorded rollout: the rows into the sim's tensor too
-        const bool mirror = t + 1 == r.steps && r.obs_step != 0;
         if (active) {
             src.compute(s, c, k_t, ib, share);
             if (!share) {  // rows the pieces do not cover: straight from the lane
                 float *grow = obs_t + row * (int64_t)OW;
                 if (canonical_slots(s, k_t)) fill_obs_fast(s, c, k_t, grow, ib);
                 else fill_obs_slow(s, c, k_t, grow, ib);
-                if (mirror) {
-                    float *srow = p.c.obs + row * (int64_t)OW;
-                    if (canonical_slots(s, k_t)) fill_obs_fast(s, c, k_t, srow, ib);
-                    else fill_obs_slow(s, c, k_t, srow, ib);
-                }
             }
         }
         const uint64_t rows = __ballot(active && share);
@@ -2421,10 +2406,7 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
                 keep[i] = idx < SR::WORDS ? ws[idx] : 0u;
             }
         }
-        // (the mirror as a second store of each piece: a second copy of the
-        // row pass in the loop body measured 1 450 -> 1 600 us per launch)
-        obs_parts<N, AUX, 0, SM>(sm, src, rows, teams, obs_t, w0 * N, lane_t, slot, k_t, active, share,
-                                 mirror ? p.c.obs : nullptr);
+        obs_parts<N, AUX, 0, SM>(sm, src, rows, teams, obs_t, w0 * N, lane_t, slot, k_t, active, share);
         __syncthreads();  // the table's readers are done
         if constexpr (SR::KEEP) {
             if (lane_used) {

@@ -21,7 +21,7 @@ enum StepMode : int {
 
 // K-step rollout (bb_rollout): step t reads actions + t*W*N*6 and writes its
 // observation rows, rewards and done flags at obs/reward/done + t*(row stride).
-// The K-step rollout kernels store the last step's rows into the sim's
+// The N = 2 K-step rollout kernels store the last step's rows into the sim's
 // observation tensor as well as the recorded buffer (instead of a copy after
 // the launch: 65 536 x 2 worlds 18.1 -> 17.3 us per step, 8 192 x 2 6.2 -> 5.55).
 struct RolloutArgs {
