@@ -93,6 +93,13 @@ def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
             "sample": f"{w} worlds x {st} steps on {threads} threads, {num_agents} agents, threefry random actions"}
 
 
+def step_loop(n_agents: int) -> bool:
+    """bb_step_n_staged runs its steps as one k_step_loop launch (the 2-agent
+    game, unless MADRONA_BB_STEP_LOOP=0)."""
+    return (n_agents <= int(os.environ.get("MADRONA_BB_STEP_LOOP_MAX_N", "2"))
+            and os.environ.get("MADRONA_BB_STEP_LOOP", "1") != "0")
+
+
 def load_traffic(workload_key: str):
     """HBM bytes per step-kernel launch from the committed PMC passes
     (tools/traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
@@ -261,6 +268,7 @@ def main():
     # least EVENT_MIN_LAUNCHES launches whatever --steps is, so the line's
     # frac is an average as long as the committed rocprof summaries'
     del staged
+    loop_main = on_gpu and not K and not args.policy and step_loop(args.agents)
     if on_gpu and (not args.policy or K):
         per_launch = K if (K and (fused or args.policy)) else 1
         ev_steps = max(args.steps, EVENT_MIN_LAUNCHES * per_launch)
@@ -273,6 +281,15 @@ def main():
         launches = ev_steps // per_launch
         avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / launches)
         del staged
+        one_launch_s = None
+        if loop_main:  # the same workload as one k_step launch per step (bb_diag_step_loop)
+            staged = sim.stage_random_actions(ev_steps, action_seed=args.seed, step0=args.warmup + args.steps + ev_steps)
+            _lib.load().bb_diag_step_loop(0)
+            barrier()
+            one_launch_s = max_over_ranks(run(staged, time_kernels=True, steps=ev_steps) / 1e3 / ev_steps)
+            barrier()
+            _lib.load().bb_diag_step_loop(-1)
+            del staged
     else:
         launches = args.steps // K if (K and fused) else args.steps
         ev_steps = args.steps
@@ -362,6 +379,15 @@ def main():
             barrier()
             k2 = max_over_ranks(go(acts2, True) / 1e3 / launches)
             barrier()
+            loop2 = step_loop(n2) and not K2
+            k1 = None
+            if loop2:  # the same steps as one k_step launch each (bb_diag_step_loop)
+                acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20 + 2 * steps2)
+                L0.bb_diag_step_loop(0)
+                barrier()
+                k1 = max_over_ranks(go(acts2, True) / 1e3 / launches)
+                barrier()
+                L0.bb_diag_step_loop(-1)
             fused2 = bool(L0.bb_rollout_fused(n2)) and K2 > 0
             if fused2:
                 # + at N = 2 the last step's rows into the sim's own tensor (recorded)
@@ -374,13 +400,18 @@ def main():
                     "steps": steps2, "value": W2 * world_size * steps2 / wall2, "unit": "env-steps/s",
                     "ms_per_step": wall2 * 1e3 / steps2,
                     "kernel": (("bb::k_rollout<%d>" if n2 == 2 else "bb::k_rollout_shared<%d>") if fused2
-                               else "bb::k_step<%d>") % n2,
-                    "launches_timed": launches, "kernel_avg_us": k2 * 1e6,
+                               else ("bb::k_step_loop<%d>" if loop2 else "bb::k_step<%d>")) % n2,
+                    "launches_timed": 1 if loop2 else launches, "kernel_avg_us": k2 * 1e6,
                     "kernel_us_per_step": k2 * 1e6 / (K2 or 1), "achieved": b2 / k2 / 1e9,
                     "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(key),
                     "algorithmic_bytes_per_launch": b2}
             if K2:
                 line["rollout"] = K2
+            if loop2:
+                line["steps_per_launch"] = steps2
+                line["kernel_avg_us_note"] = "per step: the one launch's events / its steps"
+                line["one_launch_per_step"] = {"kernel": "bb::k_step<%d>" % n2, "launches_timed": launches,
+                                               "kernel_avg_us": k1 * 1e6, "frac": b2 / k1 / 1e9 / HBM_PEAK_GBS}
             del sim2, acts2, bufs2
             torch.cuda.empty_cache()
             return line
@@ -486,7 +517,11 @@ def main():
                         f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
                         + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
                            f"of every step recorded into [{K}, W, N, ...] buffers" if K and not args.policy
-                           else ("" if K else "; one step per call"))
+                           else ("" if K else ("; the timed steps in one bb_step_n_staged call = one k_step_loop "
+                                               "launch (each wave steps its worlds once per staged step; "
+                                               "bit-identical to one k_step launch per step, the "
+                                               "one_launch_per_step object)" if loop_main
+                                               else "; one k_step launch per step")))
                         + ((f"; PPO's rollout on the device (bb_rollout_policy: per step the fused policy "
                             f"-- reference Agent layout, random init, categorical sampling -- acts for agent 0, the "
                             f"step, and obs/actions/log-probs/values/rewards/dones recorded into [{K}, W, ...] "
@@ -506,11 +541,20 @@ def main():
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": (("bb::k_rollout<%d>" if args.agents == 2 else "bb::k_rollout_shared<%d>") if (K and fused)
-                       else "bb::k_step<%d>") % args.agents,
+                       else ("bb::k_step_loop<%d>" if loop_main else "bb::k_step<%d>")) % args.agents,
             "kernel_avg_us": avg_kernel_s * 1e6,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },
     }
+    if loop_main and on_gpu:
+        # kernel_avg_us (and achieved / frac) are per step: one k_step_loop
+        # launch's events over its steps (rocprof shows the launch: x steps)
+        out["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
+        out["roofline"]["steps_per_launch"] = ev_steps
+        out["roofline"]["one_launch_per_step"] = {
+            "kernel": "bb::k_step<%d>" % args.agents, "kernel_avg_us": one_launch_s * 1e6,
+            "achieved": bytes_per_launch / one_launch_s / 1e9,
+            "frac": bytes_per_launch / one_launch_s / 1e9 / HBM_PEAK_GBS}
     if not on_gpu:
         out["roofline"] = None
         out["config"]["parallelism"] += " (host executor, gloo)"

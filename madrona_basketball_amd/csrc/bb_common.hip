@@ -412,4 +412,12 @@ hipError_t launch_init(int n, const Params &p, hipStream_t s)
 #undef CALL
 }
 
+hipError_t launch_step_loop(int n, const Params &p, int32_t *actions, int32_t steps, hipStream_t s, hipEvent_t ev0,
+                            hipEvent_t ev1)
+{
+#define CALL(k) launch_step_loop_t<k>(p, actions, steps, s, ev0, ev1)
+    BB_DISPATCH_N(n, CALL)
+#undef CALL
+}
+
 }  // namespace bb

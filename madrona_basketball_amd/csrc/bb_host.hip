@@ -689,6 +689,28 @@ int bb_fill_random_actions(bb_sim *s, int32_t *actions, int32_t n, uint32_t acti
     return BB_OK;
 }
 
+// bb_step_n_staged's steps of the 2-agent game in one k_step_loop launch
+// (default) or one k_step launch per step (MADRONA_BB_STEP_LOOP=0).
+static int g_step_loop_force = -1;  // bb_diag_step_loop: -1 by the environment, 0 off, 1 on
+static bool step_loop_enabled()
+{
+    static const bool v = [] {
+        const char *e = std::getenv("MADRONA_BB_STEP_LOOP");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return g_step_loop_force < 0 ? v : g_step_loop_force != 0;
+}
+
+// ... up to this many agents (MADRONA_BB_STEP_LOOP_MAX_N; default 2).
+static int step_loop_max_n()
+{
+    static const int v = [] {
+        const char *e = std::getenv("MADRONA_BB_STEP_LOOP_MAX_N");
+        return e && *e ? std::atoi(e) : 2;
+    }();
+    return v;
+}
+
 int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float *kernel_ms)
 {
     if (!s || n < 0 || (!actions && n > 0)) return fail(BB_ERR_INVALID_ARG, "bb_step_n_staged");
@@ -706,15 +728,24 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     }
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;
+    // the 2-agent step: the n steps in one k_step_loop launch (each wave steps
+    // its worlds n times; bit-identical to n k_step launches); otherwise, or
+    // with MADRONA_BB_STEP_LOOP=0, one k_step launch per step
+    const bool loop = n > 1 && s->n <= step_loop_max_n() && step_loop_enabled();
     std::vector<hipEvent_t> ev;
     if (kernel_ms && n > 0) {
-        ev.resize((size_t)2 * n);
+        ev.resize((size_t)2 * (loop ? 1 : n));
         for (auto &e : ev) {
             hipError_t he = hipEventCreate(&e);
             if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
         }
     }
-    for (int32_t k = 0; k < n; k++) {
+    if (loop) {
+        hipError_t e = bb::launch_step_loop(s->n, pp, actions, n, st, ev.empty() ? nullptr : ev[0],
+                                            ev.empty() ? nullptr : ev[1]);
+        if (e != hipSuccess) return hip_fail(e, "launch step loop kernel");
+    }
+    for (int32_t k = 0; k < (loop ? 0 : n); k++) {
         pp.c.action = actions + (int64_t)k * rows;
         hipError_t e = ev.empty() ? bb::launch_step(s->n, pp, st)
                                   : bb::launch_step(s->n, pp, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
@@ -729,7 +760,7 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
         hipError_t e = hipEventSynchronize(ev.back());
         if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
         double total = 0.0;
-        for (int32_t k = 0; k < n; k++) {
+        for (int32_t k = 0; k < (loop ? 1 : n); k++) {
             float ms = 0.f;
             (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
             total += ms;
@@ -1460,6 +1491,16 @@ int bb_export(bb_sim *s, int32_t export_id, void **ptr, int32_t *dtype, int32_t 
 int64_t bb_num_worlds(const bb_sim *s) { return s ? s->cfg.num_worlds : 0; }
 int32_t bb_num_agents(const bb_sim *s) { return s ? s->n : 0; }
 int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
+
+// Diagnostic (not in the public header): bb_step_n_staged's steps as one
+// k_step_loop launch (1), one k_step launch per step (0) or by the
+// environment (-1) for the calls that follow (bench's per-launch object).
+int bb_diag_step_loop(int32_t v)
+{
+    if (v < -1 || v > 1) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_loop: -1, 0 or 1");
+    g_step_loop_force = v;
+    return BB_OK;
+}
 
 // Diagnostic (not in the public header): k_rollout_split on (1), off (0) or
 // by grid size (-1) for the rollouts that follow (bit-parity tests of both).

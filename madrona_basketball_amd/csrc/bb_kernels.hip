@@ -579,14 +579,13 @@ __device__ __forceinline__ void agent_lane_obs(const World<N> &v, const Ctx &c, 
     }
 }
 
-// One lane per agent: lane = (w - w0) * N + k.
+// One lane per agent: lane = (w - w0) * N + k (blk: the wave's world group).
 template <int N, int MODE, bool LINES, bool REC = false>
-__device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile)
+__device__ __forceinline__ void step_agent_lanes(const Params &p, float *tile, int blk, int lane)
 {
     using T = StepTile<N, LINES>;
-    const int lane = threadIdx.x;
     const int k = lane % N;
-    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w0 = (int64_t)blk * (WAVE / N);
     const int64_t w = w0 + lane / N;
     const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
     const LaneAgents<N, MODE> ag{k, &p};
@@ -2148,18 +2147,17 @@ struct SharedTiled {
 // BEYOND: the step's bytes far exceed the Infinity Cache -- rows and columns
 // are stored non-temporally (see BB_SHARED_BEYOND_AUX).
 template <int N, int MODE, bool BEYOND = false>
-__device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm)
+__device__ __forceinline__ void step_shared_world(const Params &p, float *tile, SharedLds<N> &sm, int blk, int lane)
 {
     constexpr int AUX = BEYOND ? BB_SHARED_BEYOND_AUX : BB_SHARED_AUX;
     constexpr int CAUX = BEYOND ? BB_SHARED_BEYOND_COL_AUX : BB_SHARED_AUX;
     constexpr int WPW = SharedLds<N>::WPW, OW = obs_width(N);
-    const int lane = threadIdx.x;
     // lanes past WPW*N mirror agents of the last world: they run its systems
     // (identical LDS writes) but own no row and store nothing
     const bool lane_used = lane < WPW * N;
     const int slot = lane_used ? lane / N : WPW - 1;
     const int k = lane_used ? lane % N : (lane - WPW * N) % N;
-    const int64_t w0 = (int64_t)blockIdx.x * WPW;
+    const int64_t w0 = (int64_t)blk * WPW;
     const int64_t w = w0 + slot;
     const bool world_ok = w < p.num_worlds;  // uniform over the world's lanes
     const bool active = lane_used && world_ok;
@@ -2546,11 +2544,64 @@ __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
             const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
             for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
         }
-        step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm);
+        step_shared_world<N, MODE, LINES>(p, (float *)tile4, sm, (int)blockIdx.x, (int)threadIdx.x);
     } else if constexpr (Lanes<N>::LPW == N) {
-        step_agent_lanes<N, MODE, LINES, REC>(p, (float *)tile4);
+        step_agent_lanes<N, MODE, LINES, REC>(p, (float *)tile4, (int)blockIdx.x, (int)threadIdx.x);
     } else {
         step_world_lanes<N, MODE>(p, (float *)tile4);
+    }
+}
+
+// k_step_loop<2>: `steps` steps of bb_step_n_staged in one launch.  Worlds
+// are independent, so each wave runs its worlds' steps back to back -- step t
+// reads the staged action rows t (actions + t * act_step), loads the state its
+// own lanes stored at the end of step t - 1 and stores every column, the
+// observation rows, rewards and done flags, exactly as k_step -- with no kernel
+// boundary between steps: the waves drift apart and one's memory phases
+// overlap another's systems (k_rollout_ppo's structure without the policy).
+// Bit-identical to `steps` k_step launches (same code, same order per world).
+// G > 1: workgroups of G waves kept in step by a barrier after every step
+// (launch_step_loop_t picks G).
+template <int N, bool LINES, int G>
+__global__ __launch_bounds__(WAVE * G, BB_STEP_MINW) void k_step_loop(const Params p, int32_t *actions,
+                                                                      int64_t act_step, int32_t steps)
+{
+    if constexpr (N == 2 && Lanes<N>::LPW == N && !Lanes<N>::SHARED) {
+        constexpr int TF = tile_floats<N, LINES>();
+        __shared__ float4 tile4[G * TF / 4];
+        const int wave = G == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        for (int32_t t = 0; t < steps; t++) {
+            // opaque per-step copies of the indices (nothing derived from them
+            // is computed before the loop and held across it)
+            int32_t t_t = t, blk_t = (int)blockIdx.x * G + wave, lane_t = (int)threadIdx.x % WAVE;
+            __asm__ volatile("" : "+s"(t_t), "+s"(blk_t));
+            __asm__ volatile("" : "+v"(lane_t));
+            Params pt = p;
+            pt.c.action = actions + (int64_t)t_t * act_step;
+            step_agent_lanes<N, MODE_FULL, LINES, false>(pt, (float *)tile4 + wave * TF, blk_t, lane_t);
+            // this step's stores before the next step's loads (the wave's own
+            // lanes' words; same wave, same vector L1); the tile is free again
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            if constexpr (G > 1) __syncthreads();
+            else wave_sync();
+        }
+    } else if constexpr (Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value && G == 1) {
+        // N >= 4: the shared-LDS-world step (one wave per 64 / N worlds) the
+        // same way, the row decode table loaded once
+        __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
+        __shared__ SharedLds<N> sm;
+        const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
+        for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
+        for (int32_t t = 0; t < steps; t++) {
+            int32_t t_t = t, blk_t = (int)blockIdx.x, lane_t = (int)threadIdx.x;
+            __asm__ volatile("" : "+s"(t_t), "+s"(blk_t));
+            __asm__ volatile("" : "+v"(lane_t));
+            Params pt = p;
+            pt.c.action = actions + (int64_t)t_t * act_step;
+            step_shared_world<N, MODE_FULL, LINES>(pt, (float *)tile4, sm, blk_t, lane_t);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+            __syncthreads();
+        }
     }
 }
 
@@ -2597,6 +2648,55 @@ static unsigned device_cus()
         return (unsigned)cus;
     }();
     return v;
+}
+
+// k_step_loop's workgroup size for a grid of `waves` (MADRONA_BB_STEP_LOOP_G
+// = 1 / 2 / 4 forces it; read once per process).
+static int step_loop_group(int64_t waves)
+{
+    static const int forced = [] {
+        const char *e = getenv("MADRONA_BB_STEP_LOOP_G");
+        const int v = e && *e ? atoi(e) : 0;
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }();
+    if (forced) return forced;
+    return waves >= 4 * (int64_t)device_cus() ? 4 : 1;
+}
+
+template <int N>
+hipError_t launch_step_loop_t(const Params &p, int32_t *actions, int32_t steps, hipStream_t s, hipEvent_t ev0,
+                              hipEvent_t ev1)
+{
+    if constexpr (N == 2 && Lanes<N>::LPW == N && !Lanes<N>::SHARED) {
+        // 4-wave workgroups in step (a barrier per step) while the grid still
+        // gives every CU one; 1-wave workgroups drifting freely below that.
+        // Measured (profiles/r05/x_, y_): 65 536 worlds 22.6 (1) / 19.6 (4) /
+        // 20.3 (8) us per step against 21.3 with one k_step per step; 8 192
+        // 6.6 (1) / 9.9 (4; 64 CUs busy); 262 144 64.0 / 61.7 / 66.9.
+        const int64_t waves = (p.num_worlds + Lanes<N>::WPB - 1) / Lanes<N>::WPB;
+        const int g = step_loop_group(waves);
+        const dim3 grid((unsigned)((waves + g - 1) / g)), block(WAVE * g);
+        const int64_t act_step = p.num_worlds * N * 6;
+        const bool lines = step_lines<N>(p.num_worlds);
+#define BB_LOOP(L, G) hipExtLaunchKernelGGL((k_step_loop<N, L, G>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps)
+        switch (g) {
+        case 4: if (lines) BB_LOOP(true, 4); else BB_LOOP(false, 4); break;
+        case 2: if (lines) BB_LOOP(true, 2); else BB_LOOP(false, 2); break;
+        default: if (lines) BB_LOOP(true, 1); else BB_LOOP(false, 1); break;
+        }
+#undef BB_LOOP
+        return hipGetLastError();
+    } else if constexpr (Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value) {
+        constexpr int WPB = Lanes<N>::WPB;
+        const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+        const int64_t act_step = p.num_worlds * N * 6;
+        if (step_lines<N>(p.num_worlds))
+            hipExtLaunchKernelGGL((k_step_loop<N, true, 1>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps);
+        else hipExtLaunchKernelGGL((k_step_loop<N, false, 1>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps);
+        return hipGetLastError();
+    } else {
+        return hipErrorNotSupported;
+    }
 }
 
 template <int N>
@@ -2743,6 +2843,7 @@ hipError_t launch_init_t(const Params &p, hipStream_t s)
 }
 
 template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t);
+template hipError_t launch_step_loop_t<BB_N>(const Params &, int32_t *, int32_t, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRolloutArgs &, hipStream_t);

@@ -104,6 +104,10 @@ extern int force_rollout_split;
 
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
+// `steps` staged steps (actions + t * W * N * 6) in one launch (k_step_loop;
+// N = 2 only, hipErrorNotSupported otherwise)
+template <int N> hipError_t launch_step_loop_t(const Params &p, int32_t *actions, int32_t steps, hipStream_t s,
+                                               hipEvent_t ev0, hipEvent_t ev1);
 template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= waves)
 template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
                                              hipEvent_t ev1);
@@ -114,6 +118,7 @@ template <int N> hipError_t launch_rollout_policy_t(const Params &p, const Polic
 #define BB_EXTERN_N(n)                                                                  \
     extern template hipError_t launch_step_t<n>(const Params &, int, hipStream_t, hipEvent_t, hipEvent_t); \
     extern template hipError_t launch_init_t<n>(const Params &, hipStream_t);           \
+    extern template hipError_t launch_step_loop_t<n>(const Params &, int32_t *, int32_t, hipStream_t, hipEvent_t, hipEvent_t); \
     template <> int step_grid<n>(int64_t);                                              \
     extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
     template <> bool fused_rollout<n>();                                                \
@@ -129,6 +134,8 @@ BB_EXTERN_N(10)
 hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode = MODE_FULL, hipEvent_t ev0 = nullptr,
                        hipEvent_t ev1 = nullptr);
 hipError_t launch_init(int n, const Params &p, hipStream_t s);
+hipError_t launch_step_loop(int n, const Params &p, int32_t *actions, int32_t steps, hipStream_t s,
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
                           hipEvent_t ev1 = nullptr);
 bool fused_rollout_n(int n);

@@ -55,6 +55,58 @@ def test_gpu_staged_actions_equal_per_step_writes():
         assert torch.equal(a._views[name].cpu(), h._views[name]), name
 
 
+@pytest.mark.parametrize("W,n", [(65536, 40), (40001, 30), (262144, 12), (100, 25)])
+def test_gpu_staged_loop_kernel_equals_per_step_launches(W, n):
+    """bb_step_n_staged of the 2-agent game runs its n steps in one k_step_loop
+    launch (each wave steps its worlds n times): every column == n per-step
+    launches (bb_step_n), at the headline size, a ragged grid, beyond the
+    Infinity Cache (whole-line rows) and a one-wave grid."""
+    a = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    b = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    a.step_n(n, random_actions=True, action_seed=11, step0=5)
+    staged = b.stage_random_actions(n, action_seed=11, step0=5)
+    b.step_n_staged(staged)
+    torch.cuda.synchronize()
+    for name in a._views:
+        assert torch.equal(a._views[name], b._views[name]), name
+
+
+STAGED_CHILD = r"""
+import hashlib, torch
+from madrona_basketball_amd import ExecMode
+from tests.helpers import make_sim
+h = hashlib.sha256()
+for W, n, N in [(65536, 20, 2), (3001, 40, 2), (16384, 12, 4), (1000, 10, 10), (777, 12, 6)]:
+    sim = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
+    staged = sim.stage_random_actions(n, action_seed=12, step0=0)
+    sim.step_n_staged(staged)
+    torch.cuda.synchronize()
+    h.update(staged.cpu().numpy().tobytes())
+    for name in sorted(sim._views):
+        h.update(sim._views[name].cpu().numpy().tobytes())
+print("HASH", h.hexdigest())
+"""
+
+
+def test_gpu_staged_loop_kernel_write_backs():
+    """The staged action rows after the call (the defence AI's overrides written
+    back) and every column: the loop kernel == one k_step launch per step
+    (MADRONA_BB_STEP_LOOP=0, read once per process: child processes), at 2
+    agents and -- the loop forced on up to 10 agents -- the shared-world step."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for loop in ("1", "0"):
+        env = dict(os.environ, MADRONA_BB_STEP_LOOP=loop, MADRONA_BB_STEP_LOOP_MAX_N="10", PYTHONPATH=root)
+        r = subprocess.run([sys.executable, "-c", STAGED_CHILD], cwd=root, env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out[loop] = [l for l in r.stdout.splitlines() if l.startswith("HASH")][-1]
+    assert out["1"] == out["0"], out
+
+
 def test_gpu_tag_heavy_rollout():
     """Contact path (agentCollisionSystem SAT, tags, delayed resets) under a
     mostly idle offence, 4096 worlds x 800 steps vs the oracle."""

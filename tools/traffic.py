@@ -7,6 +7,9 @@ streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane
 streaming stores.  Infinity-Cache hits are counted (not excluded).
 
 python tools/traffic.py <fetch_dir> <write_dir> <workload_key> [--out profiles/traffic.json]
+python tools/traffic.py <fetch_dir> <write_dir> W65536_PPO_R32 --ppo-fused 32
+    (the fused PPO kernels: k_rollout_ppo / k_rollout_policy launches of 32
+    steps, their counters per step)
 python tools/traffic.py <fetch_dir> <write_dir> W65536_PPO_R32 --ppo 1
     (PPO rollout: every k_policy, k_step and k_step_ppo launch summed, per
     step = per step launch x the parts a step is split into -- 2 for the
@@ -57,6 +60,22 @@ def ppo_per_step(d, counter, parts, k_steps=1):
     return tot / n, pol / n, steps
 
 
+def fused_per_step(d, counter, k_steps):
+    """A fused PPO rollout (k_rollout_ppo / k_rollout_policy: k_steps steps per
+    launch; the warm-up's plain k_step launches are not PPO steps): the
+    counter summed over those launches, per step."""
+    tot, launches = 0.0, 0
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r["Counter_Name"] == counter and ("k_rollout_ppo<" in r["Kernel_Name"]
+                                                 or "k_rollout_policy<" in r["Kernel_Name"]):
+                tot += float(r["Counter_Value"])
+                launches += 1
+    if not launches:
+        raise SystemExit(f"no fused PPO {counter} rows under {d}")
+    return tot / (launches * k_steps), launches
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_dir")
@@ -69,11 +88,25 @@ def main():
     ap.add_argument("--div", type=int, default=1, help="units (steps) per launch: the entry is per unit")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "profiles", "traffic.json"))
+    ap.add_argument("--ppo-fused", type=int, default=0, help="fused PPO rollout: steps per launch")
     a = ap.parse_args()
     try:
         data = json.load(open(a.out))
     except (OSError, ValueError):
         data = {}
+    if a.ppo_fused:
+        fk, nf = fused_per_step(a.fetch_dir, "FETCH_SIZE", a.ppo_fused)
+        wk, nw = fused_per_step(a.write_dir, "WRITE_SIZE", a.ppo_fused)
+        fetch, write = 2.0 * fk * 1024.0, wk * 1024.0
+        data[a.key] = {
+            "bytes_per_launch": fetch + write, "fetch_bytes": fetch, "write_bytes": write,
+            "per": f"PPO step (fused rollout launches of {a.ppo_fused} steps: their counters / steps)",
+            "launches": [nf, nw], "correction": "FETCH_SIZE x2 (gfx950 half-count), KiB -> bytes",
+            "source": a.note,
+        }
+        json.dump(data, open(a.out, "w"), indent=1, sort_keys=True)
+        print(json.dumps(data[a.key]))
+        return
     if a.ppo:
         fk, fpol, nf = ppo_per_step(a.fetch_dir, "FETCH_SIZE", a.ppo, a.ppo_k)
         wk, wpol, nw = ppo_per_step(a.write_dir, "WRITE_SIZE", a.ppo, a.ppo_k)
