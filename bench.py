@@ -94,9 +94,9 @@ def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
 
 
 def step_loop(n_agents: int) -> bool:
-    """bb_step_n_staged runs its steps as one k_step_loop launch (the 2-agent
-    game, unless MADRONA_BB_STEP_LOOP=0)."""
-    return (n_agents <= int(os.environ.get("MADRONA_BB_STEP_LOOP_MAX_N", "2"))
+    """bb_step_n_staged runs its steps as one k_step_loop launch (unless
+    MADRONA_BB_STEP_LOOP=0 or N > MADRONA_BB_STEP_LOOP_MAX_N)."""
+    return (n_agents <= int(os.environ.get("MADRONA_BB_STEP_LOOP_MAX_N", "10"))
             and os.environ.get("MADRONA_BB_STEP_LOOP", "1") != "0")
 
 

@@ -12,6 +12,7 @@
 #   pmcro:<W>:<K>[:<N>]        FETCH_SIZE / WRITE_SIZE of bb_rollout
 #   sqppo:<W>                  SQ counters of the PPO rollout's kernels (K=32)
 #   sq:<W>:<N>                 SQ issue / wait / instruction counters of k_step<N>
+#   pmcl:<W>:<N> / sql:<W>:<N> the same of the staged-step loop (200-step launches)
 #   tests                      pytest -m gpu
 #   pytest:<file>[:<k expr>]   pytest -m gpu of one test file (optionally -k)
 #   smoke                      __graft_entry__.smoke()
@@ -60,6 +61,12 @@ for s in "$@"; do
             step "pmc_W${a}_N${b}_$c" 120 rocprofv3 --pmc $c -d "$OUT/pmc_W${a}_N${b}_$c" -o run --output-format csv \
                 -- $B --worlds "$a" --agents "$b" --steps 20 --warmup 5
          done ;;
+    pmcl) for c in FETCH_SIZE WRITE_SIZE; do  # the staged-step loop: 200-step launches
+            step "pmcl_W${a}_N${b}_$c" 180 rocprofv3 --pmc $c -d "$OUT/pmcl_W${a}_N${b}_$c" -o run --output-format csv \
+                -- $B --worlds "$a" --agents "$b" --steps 200 --warmup 5
+         done ;;
+    sql) step "sql_W${a}_N$b" 180 rocprofv3 --pmc $SQ -d "$OUT/sql_W${a}_N$b" -o run --output-format csv \
+            -- $B --worlds "$a" --agents "$b" --steps 200 --warmup 5 ;;
     pmcppo) for c in FETCH_SIZE WRITE_SIZE; do
             step "pmc_ppo_W${a}_$c" 120 rocprofv3 --pmc $c -d "$OUT/pmc_ppo_W${a}_$c" -o run --output-format csv \
                 -- $B --worlds "$a" --policy --rollout 32 --steps 64 --warmup 32
