@@ -164,7 +164,9 @@ int bb_write_random_actions(bb_sim *sim, uint32_t action_seed, uint32_t step, vo
  * actions + k * num_worlds * num_agents * 6 (layout [n][W][N][6], memory of the
  * simulator's device in CUDA mode, host memory in CPU mode) instead of the
  * action tensor; afterwards the action tensor holds step n-1's rows.
- * kernel_ms as in bb_step_n. */
+ * On gfx950 the n steps run as one launch (k_step_loop: each wave steps its
+ * worlds n times, every step's outputs written as by bb_step; identical
+ * results to n bb_step launches).  kernel_ms as in bb_step_n (the launch's). */
 int bb_step_n_staged(bb_sim *sim, int32_t n, int32_t *actions, void *stream, float *kernel_ms);
 
 /* Stage n steps of the synthetic workload of bb_step_n (steps step0..step0+n-1)
