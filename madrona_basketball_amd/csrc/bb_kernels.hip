@@ -941,7 +941,7 @@ __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, c
 
 // ------------------------------------------------------------------ PPO rollout
 // scripts/ppo.py:61-141 in one launch (bb_rollout_policy, N = 2): a workgroup
-// of 1 + PPO_PWAVES waves per 32 worlds.  Wave S holds the worlds in
+// of 1 + PW waves per 32 worlds (PW policy waves).  Wave S holds the worlds in
 // registers for all K steps (rollout_agent_lanes' discipline); the policy
 // waves P hold the network's B operands in registers (k_policy's) and own 16
 // trainee rows each.  Per step k:
@@ -965,24 +965,25 @@ __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, c
 // the loop, so their hand-offs are lds_barrier()s, which do not wait for the
 // wave's outstanding global stores (a __syncthreads() release fence does:
 // vmcnt(0) before every hand-off, ~1 us of write latency per step).
-// BB_PPO_PWAVES=4 (A/B): two policy waves per M-tile, one output half each
-// (policy_layers_half_split), accumulators exchanged through LDS for the
-// LayerNorms: 5 more workgroup barriers per step, 8 rows per bucket pass.
-#ifndef BB_PPO_PWAVES
-#define BB_PPO_PWAVES 2
-#endif
-constexpr int PPO_PWAVES = BB_PPO_PWAVES;
-constexpr int PPO_LAYER_BARS = PPO_PWAVES == 4 ? 5 : 0;
-constexpr int PPO_ROWS = 32 / PPO_PWAVES;  // rows per policy wave's bucket pass
+// PW policy waves per 32 worlds: 2 (one per M-tile) or 4 (two per M-tile,
+// one output half each: policy_layers_half_split, accumulators exchanged
+// through LDS for the LayerNorms, 5 more workgroup barriers per step, 8 rows
+// per bucket pass).  launch_rollout_policy_t picks PW.
+template <int PW>
+struct PpoCfg {
+    static constexpr int LAYER_BARS = PW == 4 ? 5 : 0;
+    static constexpr int ROWS = 32 / PW;  // rows per policy wave's bucket pass
+};
 constexpr int PPO_XS = 132;  // LDS row stride of X (floats)
+template <int PW>
 struct PpoLds {
     float x[32][PPO_XS];
     int32_t act[32][6];
     float norm[2][POL_IN];
     float ptile[2][16][33];   // each M-tile's hidden activations, then (2 waves) logits + value
-    float ltile[PPO_PWAVES == 4 ? 2 : 1][16][33];  // (4 waves) logits + value of each M-tile
-    HalfExchange ex[PPO_PWAVES == 4 ? 2 : 1];
-    BucketLds<PPO_ROWS> bucket[PPO_PWAVES];
+    float ltile[PW == 4 ? 2 : 1][16][33];  // (4 waves) logits + value of each M-tile
+    HalfExchange ex[PW == 4 ? 2 : 1];
+    BucketLds<32 / PW> bucket[PW];
     double erf[ERF_WORDS];
 };
 
@@ -1090,8 +1091,8 @@ __device__ __forceinline__ void ppo_x_pass(const World<2> &v, const Ctx &c, cons
     }
 }
 
-template <int N>
-__device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, float *tile)
+template <int N, int PW>
+__device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds<PW> &L, float *tile)
 {
     static_assert(N == 2, "the reference's 2-agent game");
     ppo_trace_wg(r, 0);
@@ -1128,7 +1129,7 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         Ctx c = make_ctx(p, w_t, k == 0);
         c.erf_tab = L.erf;
         const LaneAgents<N, MODE_FULL> ag{k, &p};
-        for (int b = 0; b < PPO_LAYER_BARS; b++) lds_barrier();  // (the policy pass's own barriers)
+        for (int b = 0; b < PpoCfg<PW>::LAYER_BARS; b++) lds_barrier();  // (the policy pass's own barriers)
         lds_barrier();  // the policy's actions are in LDS
         ppo_trace(r, t, 0);
         int32_t ib = -1;
@@ -1199,22 +1200,23 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         store_world_agent(v, p, w_s * N + k, 0);
         if (k == 0) store_world_shared(v, p, w_s);
     }
-    for (int b = 0; b < PPO_LAYER_BARS; b++) lds_barrier();  // (the next-value pass's barriers)
+    for (int b = 0; b < PpoCfg<PW>::LAYER_BARS; b++) lds_barrier();  // (the next-value pass's barriers)
     ppo_trace_wg(r, 1);
 }
 
-__device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds &L, int pw)
+template <int PW>
+__device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds<PW> &L, int pw)
 {
-    constexpr int RW = PPO_ROWS;                              // this wave's rows (bucket pass, records)
+    constexpr int RW = PpoCfg<PW>::ROWS;                              // this wave's rows (bucket pass, records)
     const int lane = threadIdx.x % WAVE, c = lane & 15, q = lane >> 4;
     const int64_t W = p.num_worlds;
-    const int m = PPO_PWAVES == 4 ? pw >> 1 : pw;             // M-tile
-    const int h = PPO_PWAVES == 4 ? pw & 1 : 0;               // (4 waves) column half
+    const int m = PW == 4 ? pw >> 1 : pw;             // M-tile
+    const int h = PW == 4 ? pw & 1 : 0;               // (4 waves) column half
     const int r0 = 16 * m;                                    // first X row of the M-tile
     const int rh = RW * h;                                    // this wave's rows of the M-tile
     const int64_t row0 = (int64_t)blockIdx.x * 32 + r0;       // the M-tile's first world
     // network constants: norm by the lanes of the policy waves, B operands per lane
-    for (int k = pw * WAVE + lane; k < POL_IN; k += PPO_PWAVES * WAVE) {
+    for (int k = pw * WAVE + lane; k < POL_IN; k += PW * WAVE) {
         L.norm[0][k] = r.w.obs_mean[k];
         L.norm[1][k] = r.w.obs_inv[k];
     }
@@ -1251,7 +1253,7 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             if (tr) ppo_trace(r, t, 7);
         };
         float (*lt)[33];
-        if constexpr (PPO_PWAVES == 4) {
+        if constexpr (PW == 4) {
             auto bar = [] { lds_barrier(); };
             policy_layers_half_split(&L.x[r0 + c][0], R, L.norm, L.ptile[m], L.ltile[m], L.ex[m], c, q, lane, h, mid,
                                      bar);
@@ -1296,15 +1298,15 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
 // MINW: waves per SIMD the register budget is sized for -- 1 while the grid
 // is one workgroup per CU (each of its 3 waves then has a SIMD to itself and
 // the sim wave keeps its world without spills), 2 above
-template <int N, int MINW>
-__global__ __launch_bounds__(WAVE * (1 + PPO_PWAVES), MINW) void k_rollout_policy(const Params p, const PolicyRolloutArgs r)
+template <int N, int MINW, int PW>
+__global__ __launch_bounds__(WAVE * (1 + PW), MINW) void k_rollout_policy(const Params p, const PolicyRolloutArgs r)
 {
     if constexpr (N == 2 && FusedRollout<N>::value) {
-        __shared__ PpoLds L;
+        __shared__ PpoLds<PW> L;
         __shared__ float4 tile4[StepTile<N, false>::FLOATS / 4];
         const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-        if (wave == 0) ppo_sim_wave<N>(p, r, L, (float *)tile4);
-        else ppo_policy_wave(p, r, L, wave - 1);
+        if (wave == 0) ppo_sim_wave<N, PW>(p, r, L, (float *)tile4);
+        else ppo_policy_wave<PW>(p, r, L, wave - 1);
     }
 }
 
@@ -2562,6 +2564,7 @@ __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
 // Bit-identical to `steps` k_step launches (same code, same order per world).
 // G > 1: workgroups of G waves kept in step by a barrier after every step
 // (launch_step_loop_t picks G).
+
 template <int N, bool LINES, int G>
 __global__ __launch_bounds__(WAVE * G, BB_STEP_MINW) void k_step_loop(const Params p, int32_t *actions,
                                                                       int64_t act_step, int32_t steps)
@@ -2788,11 +2791,22 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
     if constexpr (N != 2 || !FusedRollout<N>::value) {
         return hipErrorNotSupported;
     } else {
-        const dim3 grid((unsigned)((p.num_worlds + 31) / 32)), block(WAVE * (1 + PPO_PWAVES));
+        // 4 policy waves while the grid is at most one workgroup per CU (8 192
+        // worlds: 9.66 -> 9.48 us per step, profiles/r05/ad_pw_ab.txt), 2 above
+        // (16 384: 12.1 vs 18.2); MADRONA_BB_PPO_PWAVES = 2 / 4 forces it.
         // (3 waves: each its own SIMD; 5 waves share them -- the 256-register budget)
-        if (PPO_PWAVES == 2 && grid.x <= device_cus())
-            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 1>), grid, block, 0, s, p, r);
-        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2>), grid, block, 0, s, p, r);
+        const dim3 grid((unsigned)((p.num_worlds + 31) / 32));
+        static const int forced = [] {
+            const char *e = getenv("MADRONA_BB_PPO_PWAVES");
+            const int v = e && *e ? atoi(e) : 0;
+            return v == 2 || v == 4 ? v : 0;
+        }();
+        const int pw = forced ? forced : (grid.x <= device_cus() ? 4 : 2);
+        if (pw == 4)
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2, 4>), grid, dim3(WAVE * 5), 0, s, p, r);
+        else if (grid.x <= device_cus())
+            hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 1, 2>), grid, dim3(WAVE * 3), 0, s, p, r);
+        else hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2, 2>), grid, dim3(WAVE * 3), 0, s, p, r);
         return hipGetLastError();
     }
 }
