@@ -90,7 +90,7 @@ __device__ __forceinline__ const double *erf_table_lds()
     const double *g = &bbm::ERF_TAYLOR[0][0];
 #pragma unroll
     for (int j = 0; j < (ERF_WORDS + WAVE - 1) / WAVE; j++) {
-        const int i = j * WAVE + (int)threadIdx.x;
+        const int i = j * WAVE + (int)(threadIdx.x % WAVE);  // (every wave writes the whole table)
         if (i < ERF_WORDS) tab[i] = g[i];
     }
     return tab;
@@ -675,12 +675,12 @@ struct FusedRollout {
 };
 
 template <int N>
-__device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile)
+__device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile, int blk,
+                                                    int lane)
 {
     using T = RolloutTile<N>;
     static_assert(6 * WAVE <= T::FLOATS, "the tile parks the lanes' staged action rows");
-    const int lane = threadIdx.x;
-    const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
+    const int64_t w0 = (int64_t)blk * (WAVE / N);
     const int64_t w = w0 + lane / N;
     const bool active = w < p.num_worlds;  // uniform over the N lanes of a world
     const int64_t rows = p.num_worlds * N;  // [W][N] rows per step
@@ -783,12 +783,17 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
 // spills the step loop's state (140 B of scratch per lane, reloaded on the
 // chain every step); 1 gives the wave the SIMD's whole file (VGPRs + AGPRs,
 // no scratch) and is taken while the grid is at most one wave per SIMD.
-template <int N, int MINW = 2>
-__global__ __launch_bounds__(WAVE, MINW) void k_rollout(const Params p, const RolloutArgs r)
+// G > 1: workgroups of G waves, kept in step by the loop's two barriers per
+// step (not launched: G = 4 measured slower, 65 536 worlds 15.6-16.1 -> 16.6
+// us per step, profiles/r05/ag_rollout_g_ab.txt).
+template <int N, int MINW = 2, int G = 1>
+__global__ __launch_bounds__(WAVE * G, MINW) void k_rollout(const Params p, const RolloutArgs r)
 {
     if constexpr (FusedRollout<N>::value) {
-        __shared__ float4 tile4[RolloutTile<N>::FLOATS / 4];
-        rollout_agent_lanes<N>(p, r, (float *)tile4);
+        constexpr int TF = RolloutTile<N>::FLOATS;
+        __shared__ float4 tile4[G * TF / 4];
+        const int wave = G == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
+        rollout_agent_lanes<N>(p, r, (float *)tile4 + wave * TF, (int)blockIdx.x * G + wave, (int)(threadIdx.x % WAVE));
     }
 }
 
