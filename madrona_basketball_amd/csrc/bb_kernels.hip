@@ -2593,20 +2593,25 @@ __global__ __launch_bounds__(WAVE * G, BB_STEP_MINW) void k_step_loop(const Para
             if constexpr (G > 1) __syncthreads();
             else wave_sync();
         }
-    } else if constexpr (Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value && G == 1) {
+    } else if constexpr (Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value) {
         // N >= 4: the shared-LDS-world step (one wave per 64 / N worlds) the
-        // same way, the row decode table loaded once
-        __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
-        __shared__ SharedLds<N> sm;
+        // same way, the row decode table loaded once per wave.  (With G > 1
+        // the step's own workgroup barriers -- every one of them reached once
+        // per step by every wave, whatever its worlds -- keep the G waves in
+        // step.)
+        constexpr int TF = tile_floats<N, LINES>();
+        __shared__ float4 tile4[G * TF / 4];
+        __shared__ SharedLds<N> sm[G];
+        const int wave = G == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
         const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
-        for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
+        for (int i = (int)(threadIdx.x % WAVE); i < obs_width(N) / 4; i += WAVE) sm[wave].code[i] = g[i];
         for (int32_t t = 0; t < steps; t++) {
-            int32_t t_t = t, blk_t = (int)blockIdx.x, lane_t = (int)threadIdx.x;
+            int32_t t_t = t, blk_t = (int)blockIdx.x * G + wave, lane_t = (int)(threadIdx.x % WAVE);
             __asm__ volatile("" : "+s"(t_t), "+s"(blk_t));
             __asm__ volatile("" : "+v"(lane_t));
             Params pt = p;
             pt.c.action = actions + (int64_t)t_t * act_step;
-            step_shared_world<N, MODE_FULL, LINES>(pt, (float *)tile4, sm, blk_t, lane_t);
+            step_shared_world<N, MODE_FULL, LINES>(pt, (float *)tile4 + wave * TF, sm[wave], blk_t, lane_t);
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             __syncthreads();
         }
@@ -2695,12 +2700,16 @@ hipError_t launch_step_loop_t(const Params &p, int32_t *actions, int32_t steps, 
 #undef BB_LOOP
         return hipGetLastError();
     } else if constexpr (Lanes<N>::SHARED && BB_OBS_PIECES && !SharedTiled<N>::value) {
+        // (1-wave workgroups: 2 / 4 waves kept in step measured no faster --
+        // 65 536 x 4 55.2 / 56.2 / 56.0 us per step, x 10 245.9 / 254.9 / 260.0,
+        // profiles/r05/aj_shared_g.txt)
         constexpr int WPB = Lanes<N>::WPB;
         const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
         const int64_t act_step = p.num_worlds * N * 6;
-        if (step_lines<N>(p.num_worlds))
-            hipExtLaunchKernelGGL((k_step_loop<N, true, 1>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps);
-        else hipExtLaunchKernelGGL((k_step_loop<N, false, 1>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps);
+#define BB_LOOP(L, G) hipExtLaunchKernelGGL((k_step_loop<N, L, G>), grid, block, 0, s, ev0, ev1, 0, p, actions, act_step, steps)
+        if (step_lines<N>(p.num_worlds)) BB_LOOP(true, 1);
+        else BB_LOOP(false, 1);
+#undef BB_LOOP
         return hipGetLastError();
     } else {
         return hipErrorNotSupported;
