@@ -2582,6 +2582,7 @@ __global__ __launch_bounds__(WAVE * G, BB_STEP_MINW) void k_step_loop(const Para
             // opaque per-step copies of the indices (nothing derived from them
             // is computed before the loop and held across it)
             int32_t t_t = t, blk_t = (int)blockIdx.x * G + wave, lane_t = (int)threadIdx.x % WAVE;
+            // (without these copies: 256 VGPRs + 350-400 B of scratch per lane)
             __asm__ volatile("" : "+s"(t_t), "+s"(blk_t));
             __asm__ volatile("" : "+v"(lane_t));
             Params pt = p;
@@ -2673,7 +2674,12 @@ static int step_loop_group(int64_t waves)
         return v == 1 || v == 2 || v == 4 ? v : 0;
     }();
     if (forced) return forced;
-    return waves >= 4 * (int64_t)device_cus() ? 4 : 1;
+    // (49 152 worlds = 1.5 waves per SIMD: 4-wave workgroups leave half the CUs
+    // with one workgroup and half with two, 18.1 us per step; 2-wave ones
+    // spread evenly, 15.6)
+    const int64_t cus = device_cus();
+    if (waves < 4 * cus) return 1;
+    return waves % (4 * cus) != 0 && waves % (2 * cus) == 0 ? 2 : 4;
 }
 
 template <int N>

@@ -5,6 +5,7 @@
 # Usage: bash tools/gpu_r05.sh <tag> <step>...
 #   bench                      default bench line (all configs, CPU baselines)
 #   prof:<W>:<N>               kernel stats of k_step<N> at W worlds, that workload alone
+#   profhead                   kernel stats of the headline line's own command (default steps)
 #   profppo:<W>                kernel stats of the PPO rollout (K=32) at W worlds
 #   profro:<W>:<K>[:<N>]       kernel stats of bb_rollout (K steps per launch) at W worlds (N agents)
 #   pmc:<W>:<N>                FETCH_SIZE / WRITE_SIZE of k_step<N> (two passes)
@@ -53,6 +54,8 @@ for s in "$@"; do
     smoke) step smoke 300 python3 -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" ;;
     prof) step "prof_W${a}_N$b" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_W${a}_N$b" -o run --output-format csv \
             -- $B --worlds "$a" --agents "$b" --steps 300 --warmup 30 ;;
+    profhead) step prof_headline 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_headline" -o run --output-format csv \
+            -- python3 "$R/bench.py" --no-cpu-baseline --no-e2e --no-configs ;;
     profppo) step "prof_ppo_W$a" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ppo_W$a" -o run --output-format csv \
             -- $B --worlds "$a" --policy --rollout 32 --steps 320 --warmup 32 ;;
     profro) step "prof_ro_W${a}_R$b$sfx" 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_ro_W${a}_R$b$sfx" -o run \
