@@ -446,8 +446,9 @@ def main():
                     "value": W2 * K2 * rollouts / wall2, "unit": "env-steps/s",
                     "us_per_step": wall2 * 1e6 / (K2 * rollouts), "rollout_avg_us_events": ev * 1e3,
                     "path": {1: "k_rollout_policy (one launch per rollout)",
-                             2: "k_policy once, then k_rollout_ppo: K x (the step + the next policy pass) in "
-                                "one launch (one k_step_ppo per step with MADRONA_BB_PPO_STEP_LOOP=0)",
+                             2: "k_rollout_ppo: the first policy pass, then K x (the step + the next policy "
+                                "pass), one launch (k_policy + one k_step_ppo per step with "
+                                "MADRONA_BB_PPO_STEP_LOOP=0)",
                              3: "k_policy + k_step per step"}.get(path, str(path)),
                     "roofline": {"bound": "hbm", "scope": "whole PPO step (policy pass + world step + records)",
                                  "algorithmic_bytes_per_step": step_bytes,
