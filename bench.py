@@ -93,11 +93,21 @@ def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
             "sample": f"{w} worlds x {st} steps on {threads} threads, {num_agents} agents, threefry random actions"}
 
 
-def step_loop(n_agents: int) -> bool:
-    """bb_step_n_staged runs its steps as one k_step_loop launch (unless
-    MADRONA_BB_STEP_LOOP=0 or N > MADRONA_BB_STEP_LOOP_MAX_N)."""
-    return (n_agents <= int(os.environ.get("MADRONA_BB_STEP_LOOP_MAX_N", "10"))
-            and os.environ.get("MADRONA_BB_STEP_LOOP", "1") != "0")
+STAGED_KERNEL = {0: "bb::k_step<%d>", 1: "bb::k_step_loop<%d>"}
+
+
+def staged_kernel(path: int, n_agents: int, worlds: int) -> str:
+    """The kernel bb_step_n_staged launches (bb_step_staged_path): 2 = the
+    register-resident loop (STORE = true instances), k_rollout_split<2> while
+    its 2-wave workgroups fit two per CU, k_rollout<2, 1> while the grid is at
+    most one wave per SIMD, else k_rollout<2, 2> (launch_rollout_t)."""
+    if path != 2:
+        return STAGED_KERNEL[path] % n_agents
+    import torch
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    waves = (worlds * n_agents + 63) // 64
+    return ("bb::k_rollout_split<2, true>" if waves <= 2 * cus
+            else "bb::k_rollout<2, %d, 1, true>" % (1 if waves <= 4 * cus else 2))
 
 
 def load_traffic(workload_key: str):
@@ -268,7 +278,9 @@ def main():
     # least EVENT_MIN_LAUNCHES launches whatever --steps is, so the line's
     # frac is an average as long as the committed rocprof summaries'
     del staged
-    loop_main = on_gpu and not K and not args.policy and step_loop(args.agents)
+    L = _lib.load()
+    staged_path = int(L.bb_step_staged_path(sim._h, max(args.steps, EVENT_MIN_LAUNCHES)))
+    loop_main = on_gpu and not K and not args.policy and staged_path != 0
     if on_gpu and (not args.policy or K):
         per_launch = K if (K and (fused or args.policy)) else 1
         ev_steps = max(args.steps, EVENT_MIN_LAUNCHES * per_launch)
@@ -281,15 +293,24 @@ def main():
         launches = ev_steps // per_launch
         avg_kernel_s = max_over_ranks(kernel_ms / 1e3 / launches)
         del staged
-        one_launch_s = None
+        one_launch_s = reload_s = None
         if loop_main:  # the same workload as one k_step launch per step (bb_diag_step_loop)
             staged = sim.stage_random_actions(ev_steps, action_seed=args.seed, step0=args.warmup + args.steps + ev_steps)
-            _lib.load().bb_diag_step_loop(0)
+            L.bb_diag_step_loop(0)
             barrier()
             one_launch_s = max_over_ranks(run(staged, time_kernels=True, steps=ev_steps) / 1e3 / ev_steps)
             barrier()
-            _lib.load().bb_diag_step_loop(-1)
+            L.bb_diag_step_loop(-1)
             del staged
+            if staged_path == 2:  # and as the k_step_loop launch that reloads the state every step
+                staged = sim.stage_random_actions(ev_steps, action_seed=args.seed,
+                                                  step0=args.warmup + args.steps + 2 * ev_steps)
+                L.bb_diag_step_loop(1)
+                barrier()
+                reload_s = max_over_ranks(run(staged, time_kernels=True, steps=ev_steps) / 1e3 / ev_steps)
+                barrier()
+                L.bb_diag_step_loop(-1)
+                del staged
     else:
         launches = args.steps // K if (K and fused) else args.steps
         ev_steps = args.steps
@@ -379,7 +400,8 @@ def main():
             barrier()
             k2 = max_over_ranks(go(acts2, True) / 1e3 / launches)
             barrier()
-            loop2 = step_loop(n2) and not K2
+            path2 = int(L0.bb_step_staged_path(sim2._h, steps2)) if not K2 else 0
+            loop2 = path2 != 0
             k1 = None
             if loop2:  # the same steps as one k_step launch each (bb_diag_step_loop)
                 acts2 = sim2.stage_random_actions(steps2, action_seed=args.seed, step0=20 + 2 * steps2)
@@ -393,14 +415,17 @@ def main():
                 # + at N = 2 the last step's rows into the sim's own tensor (recorded)
                 b2 = W2 * (K2 * L0.bb_rollout_bytes_per_world_step(n2) + L0.bb_rollout_state_bytes_per_world(n2)
                            + (L0.bb_rollout_bytes_per_world_step(n2) - 32 * n2 if n2 == 2 else 0))
+            elif loop2:  # per step, of the one launch's bytes (the resident loop reads the state once)
+                b2 = L0.bb_step_staged_bytes(sim2._h, steps2) / steps2
             else:
                 b2 = L0.bb_algorithmic_bytes_per_world(n2) * W2 * (K2 or 1)
+            b1 = L0.bb_algorithmic_bytes_per_world(n2) * W2  # one k_step launch
             key = f"W{W2}_N{n2}" + (f"_R{K2}" if K2 else "")
             line = {"worlds": W2 * world_size, "worlds_per_gpu": W2, "n_gpus": world_size, "agents": n2,
                     "steps": steps2, "value": W2 * world_size * steps2 / wall2, "unit": "env-steps/s",
                     "ms_per_step": wall2 * 1e3 / steps2,
-                    "kernel": (("bb::k_rollout<%d>" if n2 == 2 else "bb::k_rollout_shared<%d>") if fused2
-                               else ("bb::k_step_loop<%d>" if loop2 else "bb::k_step<%d>")) % n2,
+                    "kernel": ((("bb::k_rollout<%d>" if n2 == 2 else "bb::k_rollout_shared<%d>") % n2) if fused2
+                               else staged_kernel(path2, n2, W2)),
                     "launches_timed": 1 if loop2 else launches, "kernel_avg_us": k2 * 1e6,
                     "kernel_us_per_step": k2 * 1e6 / (K2 or 1), "achieved": b2 / k2 / 1e9,
                     "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(key),
@@ -410,8 +435,11 @@ def main():
             if loop2:
                 line["steps_per_launch"] = steps2
                 line["kernel_avg_us_note"] = "per step: the one launch's events / its steps"
+                if path2 == 2:
+                    line["algorithmic_bytes_note"] = ("resident loop: per step B(N) less the state reads "
+                                                      "(made once per launch), bb_step_staged_bytes / steps")
                 line["one_launch_per_step"] = {"kernel": "bb::k_step<%d>" % n2, "launches_timed": launches,
-                                               "kernel_avg_us": k1 * 1e6, "frac": b2 / k1 / 1e9 / HBM_PEAK_GBS}
+                                               "kernel_avg_us": k1 * 1e6, "frac": b1 / k1 / 1e9 / HBM_PEAK_GBS}
             del sim2, acts2, bufs2
             torch.cuda.empty_cache()
             return line
@@ -482,7 +510,6 @@ def main():
 
     total_worlds = W * world_size
     value = total_worlds * args.steps / elapsed
-    L = _lib.load()
     if K and fused:
         # per launch: the state once in and out, and per step only the action
         # rows in and the recorded rows (obs, reward, done) out;
@@ -491,6 +518,8 @@ def main():
                   else L.bb_rollout_bytes_per_world_step(args.agents) - 32 * args.agents)
         bytes_per_launch = W * (K * L.bb_rollout_bytes_per_world_step(args.agents)
                                 + L.bb_rollout_state_bytes_per_world(args.agents) + mirror)
+    elif loop_main:  # per step, of the one launch's bytes
+        bytes_per_launch = L.bb_step_staged_bytes(sim._h, ev_steps) / ev_steps
     else:
         bytes_per_launch = L.bb_algorithmic_bytes_per_world(args.agents) * W
     achieved_gbs = bytes_per_launch / avg_kernel_s / 1e9
@@ -518,10 +547,14 @@ def main():
                         f"[2,8,3,2,2,2]) staged in HBM before the timed region, per-world RNG"
                         + (f"; rollouts of {K} steps per call (bb_rollout), observations/rewards/dones "
                            f"of every step recorded into [{K}, W, N, ...] buffers" if K and not args.policy
-                           else ("" if K else ("; the timed steps in one bb_step_n_staged call = one k_step_loop "
-                                               "launch (each wave steps its worlds once per staged step; "
-                                               "bit-identical to one k_step launch per step, the "
-                                               "one_launch_per_step object)" if loop_main
+                           else ("" if K else (("; the timed steps in one bb_step_n_staged call = one "
+                                                + ("k_step_loop launch (each wave steps its worlds once per "
+                                                   "staged step" if staged_path == 1 else
+                                                   "resident-loop launch (the worlds in registers between "
+                                                   "steps, every step's state columns, rows, rewards and done "
+                                                   "flags stored")
+                                                + "; bit-identical to one k_step launch per step, the "
+                                                "one_launch_per_step object)") if loop_main
                                                else "; one k_step launch per step")))
                         + ((f"; PPO's rollout on the device (bb_rollout_policy: per step the fused policy "
                             f"-- reference Agent layout, random init, categorical sampling -- acts for agent 0, the "
@@ -541,8 +574,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": (("bb::k_rollout<%d>" if args.agents == 2 else "bb::k_rollout_shared<%d>") if (K and fused)
-                       else ("bb::k_step_loop<%d>" if loop_main else "bb::k_step<%d>")) % args.agents,
+            "kernel": ((("bb::k_rollout<%d>" if args.agents == 2 else "bb::k_rollout_shared<%d>") % args.agents)
+                       if (K and fused) else staged_kernel(staged_path if loop_main else 0, args.agents, W)),
             "kernel_avg_us": avg_kernel_s * 1e6,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },
@@ -552,10 +585,20 @@ def main():
         # launch's events over its steps (rocprof shows the launch: x steps)
         out["roofline"]["algorithmic_bytes_per_step"] = bytes_per_launch
         out["roofline"]["steps_per_launch"] = ev_steps
+        b1 = L.bb_algorithmic_bytes_per_world(args.agents) * W  # one k_step launch
         out["roofline"]["one_launch_per_step"] = {
             "kernel": "bb::k_step<%d>" % args.agents, "kernel_avg_us": one_launch_s * 1e6,
-            "achieved": bytes_per_launch / one_launch_s / 1e9,
-            "frac": bytes_per_launch / one_launch_s / 1e9 / HBM_PEAK_GBS}
+            "achieved": b1 / one_launch_s / 1e9,
+            "frac": b1 / one_launch_s / 1e9 / HBM_PEAK_GBS}
+        if reload_s is not None:
+            out["roofline"]["algorithmic_bytes_note"] = (
+                "resident loop: per step B(N) less the state reads, which it makes once per launch "
+                "(bb_step_staged_bytes / steps); every step's state columns, rows, rewards, done flags "
+                "and action write-backs are stored")
+            out["roofline"]["state_reload_loop"] = {
+                "kernel": "bb::k_step_loop<%d>" % args.agents, "kernel_avg_us": reload_s * 1e6,
+                "achieved": b1 / reload_s / 1e9, "frac": b1 / reload_s / 1e9 / HBM_PEAK_GBS,
+                "what": "the same steps with every state column reloaded each step (MADRONA_BB_STEP_LOOP=1)"}
     if not on_gpu:
         out["roofline"] = None
         out["config"]["parallelism"] += " (host executor, gloo)"

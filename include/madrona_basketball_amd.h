@@ -164,10 +164,25 @@ int bb_write_random_actions(bb_sim *sim, uint32_t action_seed, uint32_t step, vo
  * actions + k * num_worlds * num_agents * 6 (layout [n][W][N][6], memory of the
  * simulator's device in CUDA mode, host memory in CPU mode) instead of the
  * action tensor; afterwards the action tensor holds step n-1's rows.
- * On gfx950 the n steps run as one launch (k_step_loop: each wave steps its
- * worlds n times, every step's outputs written as by bb_step; identical
- * results to n bb_step launches).  kernel_ms as in bb_step_n (the launch's). */
+ * On gfx950 the n steps run as one launch, every step's outputs (each state
+ * column, observation row, reward, done and action write-back) written as by
+ * bb_step; identical results to n bb_step launches.  At 2 agents the worlds
+ * stay in registers between steps (k_rollout_split / k_rollout:
+ * BB_STAGED_RESIDENT); at more, each wave steps its worlds n times reloading
+ * the state its lanes stored (k_step_loop: BB_STAGED_LOOP).
+ * MADRONA_BB_STEP_LOOP = 0 / 1 / 2 forces one launch per step / the reloading
+ * loop / the resident loop (N = 2).
+ * kernel_ms as in bb_step_n (the launch's). */
 int bb_step_n_staged(bb_sim *sim, int32_t n, int32_t *actions, void *stream, float *kernel_ms);
+
+/* The launch bb_step_n_staged makes for n steps on this simulator, and the
+ * algorithmic bytes of that call over all worlds: n B(N) per world, less the
+ * state reads of steps 1..n-1 on the resident path. */
+#define BB_STAGED_PER_STEP 0 /* one step launch per step (also: CPU mode, n < 2) */
+#define BB_STAGED_LOOP 1     /* one k_step_loop launch */
+#define BB_STAGED_RESIDENT 2 /* one k_rollout_split / k_rollout launch, state columns stored every step */
+int32_t bb_step_staged_path(const bb_sim *sim, int32_t n);
+int64_t bb_step_staged_bytes(const bb_sim *sim, int32_t n);
 
 /* Stage n steps of the synthetic workload of bb_step_n (steps step0..step0+n-1)
  * into actions[n][W][N][6] for bb_step_n_staged. */

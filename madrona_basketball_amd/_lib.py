@@ -45,7 +45,7 @@ ABI_SYMBOLS = [
     "bb_record_words", "bb_record", "bb_policy_forward", "bb_rollout_policy",
     "bb_set_action", "bb_trigger_reset", "bb_export",
     "bb_num_worlds", "bb_num_agents", "bb_exec_mode", "bb_algorithmic_bytes_per_world",
-    "bb_rollout_policy_path", "bb_rollout_policy_bytes",
+    "bb_rollout_policy_path", "bb_rollout_policy_bytes", "bb_step_staged_path", "bb_step_staged_bytes",
     "bb_rollout_fused", "bb_rollout_bytes_per_world_step", "bb_rollout_state_bytes_per_world",
     "bb_last_error",
 ]
@@ -123,6 +123,8 @@ def load():
         "bb_exec_mode": (i32, [vp]),
         "bb_algorithmic_bytes_per_world": (i64, [i32]),
         "bb_rollout_policy_path": (i32, [vp, i32, ctypes.c_uint32]),
+        "bb_step_staged_path": (i32, [vp, i32]),
+        "bb_step_staged_bytes": (i64, [vp, i32]),
         "bb_rollout_policy_bytes": (i64, [vp, i32, ctypes.c_uint32, i32]),
         "bb_rollout_fused": (i32, [i32]),
         "bb_rollout_bytes_per_world_step": (i64, [i32]),

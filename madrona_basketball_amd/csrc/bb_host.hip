@@ -689,16 +689,25 @@ int bb_fill_random_actions(bb_sim *s, int32_t *actions, int32_t n, uint32_t acti
     return BB_OK;
 }
 
-// bb_step_n_staged's steps of the 2-agent game in one k_step_loop launch
-// (default) or one k_step launch per step (MADRONA_BB_STEP_LOOP=0).
-static int g_step_loop_force = -1;  // bb_diag_step_loop: -1 by the environment, 0 off, 1 on
-static bool step_loop_enabled()
+// bb_step_n_staged's steps in one launch.  Kinds: 0 one k_step launch per
+// step; 1 one k_step_loop launch (each wave loads the state its own lanes
+// stored the step before); 2 (the 2-agent game; elsewhere 1) one k_rollout /
+// k_rollout_split launch with RolloutArgs::store_state -- the state stays in
+// registers between steps and every step stores all of its columns, rows,
+// rewards, done flags and action write-backs where k_step does.
+// MADRONA_BB_STEP_LOOP = 0 / 1 / 2 forces one; default 2 (measured faster at
+// every size, bit-identical: 8 192 x 2 6.70 -> 4.93 us per step, 65 536
+// 19.30 -> 15.76, 262 144 61.5 -> 59.8; profiles/r05/an_sweep.txt,
+// ao_sweep.txt).
+static int g_step_loop_force = -1;  // bb_diag_step_loop: -1 by the environment, else the kind
+static int step_loop_kind()
 {
-    static const bool v = [] {
+    static const int v = [] {
         const char *e = std::getenv("MADRONA_BB_STEP_LOOP");
-        return !(e && *e && std::atoi(e) == 0);
+        const int k = e && *e ? std::atoi(e) : 2;
+        return k < 0 || k > 2 ? 2 : k;
     }();
-    return g_step_loop_force < 0 ? v : g_step_loop_force != 0;
+    return g_step_loop_force >= 0 ? g_step_loop_force : v;
 }
 
 // ... up to this many agents (MADRONA_BB_STEP_LOOP_MAX_N; default: every N --
@@ -711,6 +720,34 @@ static int step_loop_max_n()
         return e && *e ? std::atoi(e) : 10;
     }();
     return v;
+}
+
+// The launch bb_step_n_staged makes for n steps (BB_STAGED_*; the host
+// executor: BB_STAGED_PER_STEP).
+static int staged_path(const bb_sim *s, int32_t n)
+{
+    if (s->cfg.exec_mode != BB_EXEC_CUDA || n < 2 || s->n > step_loop_max_n()) return BB_STAGED_PER_STEP;
+    const int k = step_loop_kind();
+    if (k == 2) return s->n == 2 && bb::fused_rollout_n(s->n) ? BB_STAGED_RESIDENT : BB_STAGED_LOOP;
+    return k == 1 ? BB_STAGED_LOOP : BB_STAGED_PER_STEP;
+}
+
+int32_t bb_step_staged_path(const bb_sim *s, int32_t n)
+{
+    if (!s || n < 0) return fail(BB_ERR_INVALID_ARG, "bb_step_staged_path");
+    return staged_path(s, n);
+}
+
+int64_t bb_step_staged_bytes(const bb_sim *s, int32_t n)
+{
+    if (!s || n < 0) return 0;
+    const int64_t B = bb_algorithmic_bytes_per_world(s->n);
+    // the state reads of B(N) (120 B per agent besides its
+    // action row, 120 B per world): the resident loop makes them once
+    const int64_t R = 120 * ((int64_t)s->n + 1);
+    const int64_t per_world = staged_path(s, n) == BB_STAGED_RESIDENT ? (int64_t)n * (B - R) + (n > 0 ? R : 0)
+                                                                       : (int64_t)n * B;
+    return per_world * s->cfg.num_worlds;
 }
 
 int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float *kernel_ms)
@@ -733,7 +770,9 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     // the 2-agent step: the n steps in one k_step_loop launch (each wave steps
     // its worlds n times; bit-identical to n k_step launches); otherwise, or
     // with MADRONA_BB_STEP_LOOP=0, one k_step launch per step
-    const bool loop = n > 1 && s->n <= step_loop_max_n() && step_loop_enabled();
+    const int kind = staged_path(s, n);
+    const bool loop = kind != BB_STAGED_PER_STEP;
+    const bool resident = kind == BB_STAGED_RESIDENT;
     std::vector<hipEvent_t> ev;
     if (kernel_ms && n > 0) {
         ev.resize((size_t)2 * (loop ? 1 : n));
@@ -742,7 +781,11 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
             if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
         }
     }
-    if (loop) {
+    if (resident) {
+        bb::RolloutArgs r{actions, s->p.c.obs, s->p.c.reward, s->p.c.done, 0, 0, n, 1};
+        hipError_t e = bb::launch_rollout(s->n, pp, r, st, ev.empty() ? nullptr : ev[0], ev.empty() ? nullptr : ev[1]);
+        if (e != hipSuccess) return hip_fail(e, "launch resident step loop kernel");
+    } else if (loop) {
         hipError_t e = bb::launch_step_loop(s->n, pp, actions, n, st, ev.empty() ? nullptr : ev[0],
                                             ev.empty() ? nullptr : ev[1]);
         if (e != hipSuccess) return hip_fail(e, "launch step loop kernel");
@@ -783,7 +826,7 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
     const int64_t rows = s->cfg.num_worlds * s->n;  // [W][N]
     const int64_t ow = bb::obs_width(s->n);
     const int64_t used_bytes = (int64_t)((bb::obs_used(s->n) + 3) / 4) * 16;  // written part of a row
-    bb::RolloutArgs r;
+    bb::RolloutArgs r{};
     r.actions = actions;
     r.obs = obs_out ? obs_out : s->p.c.obs;
     r.reward = reward_out ? reward_out : s->p.c.reward;
@@ -1495,11 +1538,12 @@ int32_t bb_num_agents(const bb_sim *s) { return s ? s->n : 0; }
 int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
 
 // Diagnostic (not in the public header): bb_step_n_staged's steps as one
-// k_step_loop launch (1), one k_step launch per step (0) or by the
-// environment (-1) for the calls that follow (bench's per-launch object).
+// register-resident rollout launch (2), one k_step_loop launch (1), one
+// k_step launch per step (0) or by the environment (-1) for the calls that
+// follow (bench's per-launch object, A/B tests).
 int bb_diag_step_loop(int32_t v)
 {
-    if (v < -1 || v > 1) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_loop: -1, 0 or 1");
+    if (v < -1 || v > 2) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_loop: -1, 0, 1 or 2");
     g_step_loop_force = v;
     return BB_OK;
 }

@@ -674,7 +674,14 @@ struct FusedRollout {
     static constexpr bool value = Lanes<N>::LPW == N && !Lanes<N>::SHARED;
 };
 
-template <int N>
+// STORE (RolloutArgs::store_state): every step also stores the state columns
+// (bb_step_n_staged's resident loop; a template parameter so the rollouts'
+// code is untouched by it).
+// (The resident loop keeps the rollout's whole-line row tile although its rows
+// stay cache-resident: k_step's 2 x 13-piece rows measured slower there,
+// 65 536 x 2 15.76 -> 18.48 us per step, 32 768 8.76 -> 10.04;
+// profiles/r05/aq_steptile_sweep.txt.)
+template <int N, bool STORE>
 __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile, int blk,
                                                     int lane)
 {
@@ -748,17 +755,27 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
             share = obs_sharable(s);
             agent_view(s, v, k);
             sys_reward_agent(v, 0, AGENT0_ID + k);
-            r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
-            r.done[(int64_t)t * r.rd_step + row] = v.done[0];
-            // the defence AI's overrides go back into the staged rows
-            bool changed = false;
+            if constexpr (STORE) {
+                // the columns of step t as k_step stores them: the action row
+                // (overrides included) into the staged rows, reward and done
+                // into the sim's columns (r.reward / r.done here)
+                Params ps = p;
+                ps.c.action = act_t;
+                store_world_agent(v, ps, row, 0);
+                if (k == 0) store_world_shared(v, p, w_t);
+            } else {
+                r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
+                r.done[(int64_t)t * r.rd_step + row] = v.done[0];
+                // the defence AI's overrides go back into the staged rows
+                bool changed = false;
 #pragma unroll
-            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
-            if (changed) {
-                uint32_t a[6];
+                for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
+                if (changed) {
+                    uint32_t a[6];
 #pragma unroll
-                for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
-                store_words<6>(act_t, row, a);
+                    for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
+                    store_words<6>(act_t, row, a);
+                }
             }
         }
         __syncthreads();  // parked rows read before the tile is rewritten
@@ -770,7 +787,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
 #endif
         __syncthreads();  // the tile is rewritten by the next step
     }
-    if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
+    if (!STORE && active && r.steps > 0) {  // the simulator's own columns: state after the last step
         int64_t w_s = w;
         __asm__ volatile("" : "+v"(w_s));
         const int k = lane % N;
@@ -786,14 +803,15 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
 // G > 1: workgroups of G waves, kept in step by the loop's two barriers per
 // step (not launched: G = 4 measured slower, 65 536 worlds 15.6-16.1 -> 16.6
 // us per step, profiles/r05/ag_rollout_g_ab.txt).
-template <int N, int MINW = 2, int G = 1>
+template <int N, int MINW = 2, int G = 1, bool STORE = false>
 __global__ __launch_bounds__(WAVE * G, MINW) void k_rollout(const Params p, const RolloutArgs r)
 {
     if constexpr (FusedRollout<N>::value) {
         constexpr int TF = RolloutTile<N>::FLOATS;
         __shared__ float4 tile4[G * TF / 4];
         const int wave = G == 1 ? 0 : __builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE);
-        rollout_agent_lanes<N>(p, r, (float *)tile4 + wave * TF, (int)blockIdx.x * G + wave, (int)(threadIdx.x % WAVE));
+        rollout_agent_lanes<N, STORE>(p, r, (float *)tile4 + wave * TF, (int)blockIdx.x * G + wave,
+                                      (int)(threadIdx.x % WAVE));
     }
 }
 
@@ -814,7 +832,7 @@ struct SplitView {
     uint32_t w[WORDS][WAVE];  // word-major: word i of lane l at w[i][l]
 };
 
-template <int N>
+template <int N, bool STORE>
 __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArgs &r, SplitView<N> &view,
                                                uint32_t *park_base)
 {
@@ -864,16 +882,23 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
             share = obs_sharable(s);
             agent_view(s, v, k);
             sys_reward_agent(v, 0, AGENT0_ID + k);
-            r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
-            r.done[(int64_t)t * r.rd_step + row] = v.done[0];
-            bool changed = false;
+            if constexpr (STORE) {  // as in rollout_agent_lanes
+                Params ps = p;
+                ps.c.action = act_t;
+                store_world_agent(v, ps, row, 0);
+                if (k == 0) store_world_shared(v, p, w_t);
+            } else {
+                r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
+                r.done[(int64_t)t * r.rd_step + row] = v.done[0];
+                bool changed = false;
 #pragma unroll
-            for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
-            if (changed) {
-                uint32_t a[6];
+                for (int q = 0; q < 6; q++) changed |= (uint32_t)v.act[0][q] != park[q * WAVE];
+                if (changed) {
+                    uint32_t a[6];
 #pragma unroll
-                for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
-                store_words<6>(act_t, row, a);
+                    for (int q = 0; q < 6; q++) a[q] = (uint32_t)v.act[0][q];
+                    store_words<6>(act_t, row, a);
+                }
             }
         }
         lds_barrier();  // A: the observation wave has read view(t-1)
@@ -887,7 +912,7 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
         }
         lds_barrier();  // B: view(t) is in LDS
     }
-    if (active && r.steps > 0) {  // the simulator's own columns: state after the last step
+    if (!STORE && active && r.steps > 0) {  // the simulator's own columns: state after the last step
         int64_t w_s = w;
         __asm__ volatile("" : "+v"(w_s));
         const int k = lane % N;
@@ -896,11 +921,10 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
     }
 }
 
-template <int N>
+template <int N, class T>
 __device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArgs &r, const SplitView<N> &view,
                                                float *tile)
 {
-    using T = RolloutTile<N>;
     const int lane = (int)threadIdx.x % WAVE;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
     for (int t = 0; t < r.steps; t++) {
@@ -932,15 +956,16 @@ __device__ __forceinline__ void split_obs_wave(const Params &p, const RolloutArg
     }
 }
 
-template <int N>
+template <int N, bool STORE = false>
 __global__ __launch_bounds__(2 * WAVE, 1) void k_rollout_split(const Params p, const RolloutArgs r)
 {
     if constexpr (FusedRollout<N>::value) {
+        using T = RolloutTile<N>;
         __shared__ SplitView<N> view;
-        __shared__ float4 tile4[RolloutTile<N>::FLOATS / 4];
+        __shared__ float4 tile4[T::FLOATS / 4];
         __shared__ uint32_t park[6 * WAVE];
-        if (__builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE) == 0) split_sim_wave<N>(p, r, view, park);
-        else split_obs_wave<N>(p, r, view, (float *)tile4);
+        if (__builtin_amdgcn_readfirstlane((int)threadIdx.x / WAVE) == 0) split_sim_wave<N, STORE>(p, r, view, park);
+        else split_obs_wave<N, T>(p, r, view, (float *)tile4);
     }
 }
 
@@ -2795,9 +2820,18 @@ hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s
     } else {
         constexpr int WPB = Lanes<N>::WPB;
         const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-        if (rollout_split(grid.x))
+        const bool split = rollout_split(grid.x), minw1 = rollout_minw1(grid.x);
+        if (r.store_state) {  // bb_step_n_staged's resident loop
+            if (r.reward != p.c.reward || r.done != p.c.done || r.rd_step != 0) return hipErrorInvalidValue;
+            if (split)
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N, true>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
+            else if (minw1)
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1, 1, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
+            else
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2, 1, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        } else if (split)
             hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
-        else if (rollout_minw1(grid.x))
+        else if (minw1)
             hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1>), grid, block, 0, s, ev0, ev1, 0, p, r);
         else
             hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2>), grid, block, 0, s, ev0, ev1, 0, p, r);

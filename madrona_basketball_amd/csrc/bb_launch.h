@@ -32,6 +32,12 @@ struct RolloutArgs {
     int64_t obs_step;  // floats between consecutive steps' obs (0: one buffer for all steps)
     int64_t rd_step;   // floats between consecutive steps' reward/done (0: likewise)
     int32_t steps;     // K
+    // bb_step_n_staged's register-resident loop: every step also stores the
+    // state columns, so each step leaves in memory exactly what a k_step launch
+    // would (the state itself stays in registers between steps).  Then reward
+    // and done must be the sim's own columns (rd_step 0): they are stored with
+    // the state; the action rows are stored whole into actions[t], as k_step.
+    int32_t store_state;
 };
 
 // PPO rollout with the policy in the loop (bb_rollout_policy, fused kernel

@@ -55,17 +55,28 @@ def test_gpu_staged_actions_equal_per_step_writes():
         assert torch.equal(a._views[name].cpu(), h._views[name]), name
 
 
-@pytest.mark.parametrize("W,n", [(65536, 40), (40001, 30), (262144, 12), (100, 25)])
-def test_gpu_staged_loop_kernel_equals_per_step_launches(W, n):
-    """bb_step_n_staged of the 2-agent game runs its n steps in one k_step_loop
-    launch (each wave steps its worlds n times): every column == n per-step
-    launches (bb_step_n), at the headline size, a ragged grid, beyond the
-    Infinity Cache (whole-line rows) and a one-wave grid."""
+@pytest.mark.parametrize("kind", [1, 2])
+@pytest.mark.parametrize("W,n", [(65536, 40), (40001, 30), (262144, 12), (100, 25), (8192, 33), (32768, 21),
+                                 (20000, 17)])
+def test_gpu_staged_loop_kernel_equals_per_step_launches(W, n, kind):
+    """bb_step_n_staged of the 2-agent game runs its n steps in one launch --
+    kind 1 k_step_loop (each wave steps its worlds n times, reloading the state
+    its lanes stored), kind 2 the register-resident rollout kernels with every
+    step's state stores (k_rollout_split / k_rollout<2, 1> / k_rollout<2, 2>
+    by grid size) -- and every column == n per-step launches (bb_step_n), at
+    the headline size, ragged grids, beyond the Infinity Cache (whole-line
+    rows), a one-wave grid and the two-wave-workgroup range."""
+    from madrona_basketball_amd import _lib
+    L = _lib.load()
     a = make_sim(ExecMode.CUDA, W, per_world_rng=True)
     b = make_sim(ExecMode.CUDA, W, per_world_rng=True)
     a.step_n(n, random_actions=True, action_seed=11, step0=5)
     staged = b.stage_random_actions(n, action_seed=11, step0=5)
-    b.step_n_staged(staged)
+    assert L.bb_diag_step_loop(kind) == 0
+    try:
+        b.step_n_staged(staged)
+    finally:
+        L.bb_diag_step_loop(-1)
     torch.cuda.synchronize()
     for name in a._views:
         assert torch.equal(a._views[name], b._views[name]), name
@@ -90,21 +101,22 @@ print("HASH", h.hexdigest())
 
 def test_gpu_staged_loop_kernel_write_backs():
     """The staged action rows after the call (the defence AI's overrides written
-    back) and every column: the loop kernel == one k_step launch per step
-    (MADRONA_BB_STEP_LOOP=0, read once per process: child processes), at 2
-    agents and -- the loop forced on up to 10 agents -- the shared-world step."""
+    back) and every column: the register-resident loop (MADRONA_BB_STEP_LOOP=2)
+    and k_step_loop (1) == one k_step launch per step (0; read once per
+    process: child processes), at 2 agents and -- the loop forced on up to 10
+    agents -- the shared-world step."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = {}
-    for loop in ("1", "0"):
+    for loop in ("2", "1", "0"):
         env = dict(os.environ, MADRONA_BB_STEP_LOOP=loop, MADRONA_BB_STEP_LOOP_MAX_N="10", PYTHONPATH=root)
         r = subprocess.run([sys.executable, "-c", STAGED_CHILD], cwd=root, env=env, capture_output=True, text=True,
                            timeout=240)
         assert r.returncode == 0, r.stderr[-3000:]
         out[loop] = [l for l in r.stdout.splitlines() if l.startswith("HASH")][-1]
-    assert out["1"] == out["0"], out
+    assert out["2"] == out["0"] and out["1"] == out["0"], out
 
 
 def test_gpu_tag_heavy_rollout():
