@@ -103,6 +103,8 @@ def staged_kernel(path: int, n_agents: int, worlds: int) -> str:
     most one wave per SIMD, else k_rollout<2, 2> (launch_rollout_t)."""
     if path != 2:
         return STAGED_KERNEL[path] % n_agents
+    if n_agents != 2:
+        return "bb::k_rollout_shared<%d, true, false>" % n_agents
     import torch
     cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
     waves = (worlds * n_agents + 63) // 64

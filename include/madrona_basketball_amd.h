@@ -166,12 +166,13 @@ int bb_write_random_actions(bb_sim *sim, uint32_t action_seed, uint32_t step, vo
  * action tensor; afterwards the action tensor holds step n-1's rows.
  * On gfx950 the n steps run as one launch, every step's outputs (each state
  * column, observation row, reward, done and action write-back) written as by
- * bb_step; identical results to n bb_step launches.  At 2 agents the worlds
- * stay in registers between steps (k_rollout_split / k_rollout:
- * BB_STAGED_RESIDENT); at more, each wave steps its worlds n times reloading
- * the state its lanes stored (k_step_loop: BB_STAGED_LOOP).
- * MADRONA_BB_STEP_LOOP = 0 / 1 / 2 forces one launch per step / the reloading
- * loop / the resident loop (N = 2).
+ * bb_step; identical results to n bb_step launches.  At 2 agents, and at
+ * more while a step's bytes stay in the Infinity Cache, the worlds stay on
+ * the chip between steps (registers: k_rollout_split / k_rollout; LDS from 4
+ * agents: k_rollout_shared; BB_STAGED_RESIDENT); otherwise each wave steps its
+ * worlds n times reloading the state its lanes stored (k_step_loop:
+ * BB_STAGED_LOOP).  MADRONA_BB_STEP_LOOP = 0 / 1 / 2 forces one launch per
+ * step / the reloading loop / the resident loop where it exists.
  * kernel_ms as in bb_step_n (the launch's). */
 int bb_step_n_staged(bb_sim *sim, int32_t n, int32_t *actions, void *stream, float *kernel_ms);
 

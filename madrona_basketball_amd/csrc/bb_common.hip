@@ -332,6 +332,18 @@ hipError_t launch_step(int n, const Params &p, hipStream_t s, int mode, hipEvent
 #undef CALL
 }
 
+bool resident_staged_n(int n, int64_t num_worlds)
+{
+    switch (n) {
+    case 2: return resident_staged<2>(num_worlds);
+    case 4: return resident_staged<4>(num_worlds);
+    case 6: return resident_staged<6>(num_worlds);
+    case 8: return resident_staged<8>(num_worlds);
+    case 10: return resident_staged<10>(num_worlds);
+    default: return false;
+    }
+}
+
 int step_grid_n(int n, int64_t num_worlds)
 {
 #define CALL(k) step_grid<k>(num_worlds)

@@ -722,13 +722,27 @@ static int step_loop_max_n()
     return v;
 }
 
+// ... the resident loop up to this many agents (MADRONA_BB_STEP_RESIDENT_MAX_N;
+// default 10: from N = 4 on k_rollout_shared's resident instances, taken while
+// the step stays in the Infinity Cache, bb::resident_staged)
+static int resident_max_n()
+{
+    static const int v = [] {
+        const char *e = std::getenv("MADRONA_BB_STEP_RESIDENT_MAX_N");
+        return e && *e ? std::atoi(e) : 10;
+    }();
+    return v;
+}
+
 // The launch bb_step_n_staged makes for n steps (BB_STAGED_*; the host
 // executor: BB_STAGED_PER_STEP).
 static int staged_path(const bb_sim *s, int32_t n)
 {
     if (s->cfg.exec_mode != BB_EXEC_CUDA || n < 2 || s->n > step_loop_max_n()) return BB_STAGED_PER_STEP;
     const int k = step_loop_kind();
-    if (k == 2) return s->n == 2 && bb::fused_rollout_n(s->n) ? BB_STAGED_RESIDENT : BB_STAGED_LOOP;
+    if (k == 2)
+        return s->n <= resident_max_n() && bb::resident_staged_n(s->n, s->cfg.num_worlds) ? BB_STAGED_RESIDENT
+                                                                                          : BB_STAGED_LOOP;
     return k == 1 ? BB_STAGED_LOOP : BB_STAGED_PER_STEP;
 }
 

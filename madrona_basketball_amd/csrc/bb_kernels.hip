@@ -2347,12 +2347,17 @@ struct SharedRollout {
     using Lds = typename std::conditional<KEEP, SharedLds<N>, SharedLdsRoll<N>>::type;
 };
 
-template <int N, class SM>
+// STORE: bb_step_n_staged's resident loop (RolloutArgs::store_state) -- every
+// step stores the state columns with k_step_shared's cache policies (BEYOND:
+// the step's bytes exceed the Infinity Cache), rows into the sim's tensor.
+template <int N, class SM, bool STORE = false, bool BEYOND = false>
 __device__ __forceinline__ void rollout_shared_world(const Params &p, const RolloutArgs &r, SM &sm)
 {
     using SR = SharedRollout<N>;
     constexpr int WPW = SM::WPW, OW = obs_width(N);
-    constexpr int AUX = BB_ROLLOUT_AUX;  // rows into a fresh [K][W][N][OBSW] buffer
+    // rows into a fresh [K][W][N][OBSW] buffer, or (STORE) as the step's
+    constexpr int AUX = !STORE ? BB_ROLLOUT_AUX : (BEYOND ? BB_SHARED_BEYOND_AUX : BB_SHARED_AUX);
+    constexpr int CAUX = BEYOND ? BB_SHARED_BEYOND_COL_AUX : BB_SHARED_AUX;
     const int lane = threadIdx.x;
     const bool lane_used = lane < WPW * N;
     const int slot = lane_used ? lane / N : WPW - 1;
@@ -2403,12 +2408,22 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
         if (lane_used) s.rew[k_t] = rw;
         __syncthreads();
         if (active) {
-            uint32_t a6[6];
+            if constexpr (STORE) {
+                // every column of step t as k_step stores it: the action row
+                // (overrides included) into actions[t], reward / done into the
+                // sim's columns (r.reward / r.done here)
+                Params ps = p;
+                ps.c.action = acts;
+                store_world_agent<N, CAUX>(s, ps, row, k_t);
+                if (k_t == 0) store_world_shared<N, CAUX>(s, p, w_t);
+            } else {
+                uint32_t a6[6];
 #pragma unroll
-            for (int q = 0; q < 6; q++) a6[q] = (uint32_t)s.act[k_t][q];
-            store_words<6>(acts, row, a6);  // with the defence AI's overrides
-            r.reward[(int64_t)t * r.rd_step + row] = s.rew[k_t];
-            r.done[(int64_t)t * r.rd_step + row] = s.done[k_t];
+                for (int q = 0; q < 6; q++) a6[q] = (uint32_t)s.act[k_t][q];
+                store_words<6>(acts, row, a6);  // with the defence AI's overrides
+                r.reward[(int64_t)t * r.rd_step + row] = s.rew[k_t];
+                r.done[(int64_t)t * r.rd_step + row] = s.done[k_t];
+            }
         }
         // observation rows of step t
         float *obs_t = r.obs + (int64_t)t * r.obs_step;
@@ -2452,7 +2467,7 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
     }
     // the state after the last step, every column (the per-step launches'
     // last stores; actions / rewards / done flags as the last step left them)
-    if (active) {
+    if (!STORE && active) {
         // (opaque copies: the column addresses are not shared with the loads
         // before the loop and held across it)
         int k_e = k;
@@ -2464,14 +2479,14 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
     }
 }
 
-template <int N>
+template <int N, bool STORE = false, bool BEYOND = false>
 __global__ __launch_bounds__(WAVE, 2) void k_rollout_shared(const Params p, const RolloutArgs r)
 {
     if constexpr (SharedRollout<N>::value) {
         __shared__ typename SharedRollout<N>::Lds sm;
         const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
         for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
-        rollout_shared_world<N>(p, r, sm);
+        rollout_shared_world<N, typename SharedRollout<N>::Lds, STORE, BEYOND>(p, r, sm);
     }
 }
 
@@ -2813,7 +2828,15 @@ hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s
     if constexpr (SharedRollout<N>::value) {
         constexpr int WPB = Lanes<N>::WPB;
         const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-        hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        if (r.store_state) {  // bb_step_n_staged's resident loop
+            if (r.reward != p.c.reward || r.done != p.c.done || r.rd_step != 0) return hipErrorInvalidValue;
+            if (step_lines<N>(p.num_worlds))
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N, true, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
+            else
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N, true, false>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        } else {
+            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        }
         return hipGetLastError();
     } else if constexpr (!FusedRollout<N>::value) {
         return hipErrorNotSupported;
@@ -2917,6 +2940,15 @@ template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, 
 template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value || SharedRollout<BB_N>::value; }
 template <> bool step_records_t<BB_N>() { return BB_N == 2 && Lanes<BB_N>::LPW == BB_N && !Lanes<BB_N>::SHARED; }
+// At 2 agents always; the shared-world kernel while the step stays in the
+// Infinity Cache (65 536 x 4 52.4 -> 48.3 us per step; beyond it the
+// reloading loop is faster, 131 072 x 4 96.3 vs 114.7; profiles/r05/ar_sweep.txt).
+template <> bool resident_staged<BB_N>(int64_t num_worlds)
+{
+    if constexpr (FusedRollout<BB_N>::value) return true;
+    else if constexpr (SharedRollout<BB_N>::value) return !step_lines<BB_N>(num_worlds);
+    else return false;
+}
 template <> int step_grid<BB_N>(int64_t num_worlds)
 {
     return (int)((num_worlds + Lanes<BB_N>::WPB - 1) / Lanes<BB_N>::WPB);  // waves of the MODE_FULL launch

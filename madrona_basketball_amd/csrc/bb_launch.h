@@ -118,6 +118,8 @@ template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= wav
 template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
                                              hipEvent_t ev1);
 template <int N> bool fused_rollout();  // k_rollout<N> exists (else: one k_step launch per step)
+// bb_step_n_staged's register-resident loop (RolloutArgs::store_state) is taken
+template <int N> bool resident_staged(int64_t num_worlds);
 template <int N> bool step_records_t();  // k_step<N> honours Params::rec_obs
 template <int N> hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, hipStream_t s);
 
@@ -128,6 +130,7 @@ template <int N> hipError_t launch_rollout_policy_t(const Params &p, const Polic
     template <> int step_grid<n>(int64_t);                                              \
     extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
     template <> bool fused_rollout<n>();                                                \
+    template <> bool resident_staged<n>(int64_t);                                       \
     template <> bool step_records_t<n>();                                               \
     extern template hipError_t launch_rollout_policy_t<n>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 BB_EXTERN_N(2)
@@ -145,6 +148,7 @@ hipError_t launch_step_loop(int n, const Params &p, int32_t *actions, int32_t st
 hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
                           hipEvent_t ev1 = nullptr);
 bool fused_rollout_n(int n);
+bool resident_staged_n(int n, int64_t num_worlds);
 // whether k_step honours Params::rec_obs (PPO's buffer.obs record from the
 // step's row passes): the agent-lane kernel of the 2-agent game only
 bool step_records(int n);

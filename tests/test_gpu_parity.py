@@ -87,7 +87,8 @@ import hashlib, torch
 from madrona_basketball_amd import ExecMode
 from tests.helpers import make_sim
 h = hashlib.sha256()
-for W, n, N in [(65536, 20, 2), (3001, 40, 2), (16384, 12, 4), (1000, 10, 10), (777, 12, 6)]:
+for W, n, N in [(65536, 20, 2), (3001, 40, 2), (16384, 12, 4), (65536, 6, 4), (1000, 10, 10), (777, 12, 6),
+                (5000, 9, 8)]:
     sim = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
     staged = sim.stage_random_actions(n, action_seed=12, step0=0)
     sim.step_n_staged(staged)
