@@ -680,7 +680,10 @@ struct FusedRollout {
 // (The resident loop keeps the rollout's whole-line row tile although its rows
 // stay cache-resident: k_step's 2 x 13-piece rows measured slower there,
 // 65 536 x 2 15.76 -> 18.48 us per step, 32 768 8.76 -> 10.04;
-// profiles/r05/aq_steptile_sweep.txt.)
+// profiles/r05/aq_steptile_sweep.txt.  It stores every state column every
+// step: the event-only words parked in LDS so as to store those columns only
+// when changed, as k_step does, measured slower too, 65 536 x 2 15.76 ->
+// 17.07, 262 144 59.8 -> 65.4; profiles/r05/at_event_orig_sweep.txt.)
 template <int N, bool STORE>
 __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const RolloutArgs &r, float *tile, int blk,
                                                     int lane)
