@@ -680,7 +680,9 @@ struct FusedRollout {
 // (The resident loop keeps the rollout's whole-line row tile although its rows
 // stay cache-resident: k_step's 2 x 13-piece rows measured slower there,
 // 65 536 x 2 15.76 -> 18.48 us per step, 32 768 8.76 -> 10.04;
-// profiles/r05/aq_steptile_sweep.txt.  It stores every state column every
+// profiles/r05/aq_steptile_sweep.txt; two whole lines then the rest of the
+// used row -- one partial line per row, no zero tail -- 15.76 -> 16.96,
+// aw_linetile_sweep.txt.  It stores every state column every
 // step: the event-only words parked in LDS so as to store those columns only
 // when changed, as k_step does, measured slower too, 65 536 x 2 15.76 ->
 // 17.07, 262 144 59.8 -> 65.4; profiles/r05/at_event_orig_sweep.txt.)
