@@ -51,6 +51,9 @@ constexpr int WAVE = 64;
 #ifndef BB_LINES_AUX
 #define BB_LINES_AUX 2  // k_step, state beyond the Infinity Cache
 #endif
+#ifndef BB_RESIDENT_COL_AUX
+#define BB_RESIDENT_COL_AUX -1  // the resident staged loop's state columns (A/B)
+#endif
 #ifndef BB_ROLLOUT_AUX
 #define BB_ROLLOUT_AUX 2  // k_rollout: rows into a fresh K-step buffer
 #endif
@@ -766,8 +769,8 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
                 // into the sim's columns (r.reward / r.done here)
                 Params ps = p;
                 ps.c.action = act_t;
-                store_world_agent(v, ps, row, 0);
-                if (k == 0) store_world_shared(v, p, w_t);
+                store_world_agent<N, BB_RESIDENT_COL_AUX>(v, ps, row, 0);
+                if (k == 0) store_world_shared<N, BB_RESIDENT_COL_AUX>(v, p, w_t);
             } else {
                 r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
                 r.done[(int64_t)t * r.rd_step + row] = v.done[0];
@@ -890,8 +893,8 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
             if constexpr (STORE) {  // as in rollout_agent_lanes
                 Params ps = p;
                 ps.c.action = act_t;
-                store_world_agent(v, ps, row, 0);
-                if (k == 0) store_world_shared(v, p, w_t);
+                store_world_agent<N, BB_RESIDENT_COL_AUX>(v, ps, row, 0);
+                if (k == 0) store_world_shared<N, BB_RESIDENT_COL_AUX>(v, p, w_t);
             } else {
                 r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
                 r.done[(int64_t)t * r.rd_step + row] = v.done[0];
