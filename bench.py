@@ -1,7 +1,9 @@
 """Throughput benchmark of the MI355X basketball step (BASELINE.json metric).
 
 python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds 65536] [--agents 2]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Multi-GPU: python bench.py --gpus N starts N ranks itself (one process per
+GPU); under a launcher (python -m torch.distributed.run --nproc-per-node N ...
+bench.py --gpus N) --gpus must equal WORLD_SIZE.
 
 A "step" = one step of every world on this GPU, reading that step's
 synthetic random actions (the stand-in for the Python `actions[:] = ...` of
@@ -125,6 +127,41 @@ def load_traffic(workload_key: str):
         return None
 
 
+def launch_ranks(n: int) -> int:
+    """`--gpus N` (N > 1) without a launcher: start N ranks of this same
+    command as child processes, one per GPU (RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* in their environment, as torch.distributed.run would set them).
+    This parent never imports torch, so it never touches a GPU; it waits for
+    the ranks, stops the others if one fails, and returns the first failing
+    rank's exit status (0 when all succeed).  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                log(f"bench.py: rank {procs.index(p)} exited with status {code}; stopping the other ranks")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -160,7 +197,14 @@ def main():
     ap.add_argument("--exec", choices=["cuda", "cpu"], default="cuda",
                     help="cpu = host executor + gloo (tests of the multi-rank path)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world_size} rank(s) "
+                         "(WORLD_SIZE); they must agree")
     rank = int(os.environ.get("RANK", "0"))
     cpu = cpu_exec = None
     if rank == 0 and not args.no_cpu_baseline:  # before any GPU call (the other ranks wait at init)

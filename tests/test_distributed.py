@@ -46,6 +46,32 @@ def test_bench_two_ranks_gloo():
     assert out["e2e"]["value"] > 0  # the env.py loop, max over ranks
 
 
+def test_bench_starts_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher starts two ranks itself (one
+    process per device, RANK / WORLD_SIZE set by the parent) and rank 0 prints
+    one line with the whole job's n_gpus."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="1", BB_CPU_THREADS="2")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--exec", "cpu", "--worlds", "256",
+           "--steps", "10", "--warmup", "2", "--no-cpu-baseline", "--no-e2e"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["total_worlds"] == 512 and out["value"] > 0
+    assert "world-sharded x2" in out["config"]["parallelism"]
+
+
+def test_bench_rejects_gpus_other_than_world_size():
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(free_port()))
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--exec", "cpu", "--worlds", "64",
+           "--steps", "2", "--warmup", "0", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert r.returncode != 0 and "--gpus 3" in r.stderr and "WORLD_SIZE" in r.stderr
+
+
 def _worker(rank, world, port, W, steps, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
