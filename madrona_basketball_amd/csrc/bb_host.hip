@@ -599,27 +599,12 @@ int bb_destroy(bb_sim *s)
     return BB_OK;
 }
 
-// The per-call step (bb_step, bb_step_n, and one launch per step of
-// bb_step_n_staged): k_step, or with g_step_kernel == 1 the resident loop's
-// kernel for one step (its action rows read from and written back into
-// pp.c.action, reward / done / rows into the sim's own columns).
-static int g_step_kernel = 0;
-static hipError_t launch_one_step(const bb_sim *s, const bb::Params &pp, hipStream_t st, hipEvent_t ev0 = nullptr,
-                                  hipEvent_t ev1 = nullptr)
-{
-    if (g_step_kernel == 1 && !pp.rec_obs && bb::resident_staged_n(s->n, s->cfg.num_worlds)) {
-        bb::RolloutArgs r{pp.c.action, pp.c.obs, pp.c.reward, pp.c.done, 0, 0, 1, 1};
-        return bb::launch_rollout(s->n, pp, r, st, ev0, ev1);
-    }
-    return bb::launch_step(s->n, pp, st, bb::MODE_FULL, ev0, ev1);
-}
-
 int bb_step(bb_sim *s, void *stream)
 {
     if (!s) return fail(BB_ERR_INVALID_ARG, "sim is NULL");
     if (s->cfg.exec_mode == BB_EXEC_CUDA) {
         DeviceGuard g(s->device);
-        hipError_t e = launch_one_step(s, s->p, (hipStream_t)stream);
+        hipError_t e = bb::launch_step(s->n, s->p, (hipStream_t)stream);
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
         return BB_OK;
     }
@@ -665,7 +650,8 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
             if (e != hipSuccess) return hip_fail(e, "launch random-action kernel");
         }
         // kernel_ms: the step kernel's own start/end (hipExtLaunchKernel events)
-        hipError_t e = ev.empty() ? launch_one_step(s, s->p, st) : launch_one_step(s, s->p, st, ev[2 * k], ev[2 * k + 1]);
+        hipError_t e = ev.empty() ? bb::launch_step(s->n, s->p, st)
+                                  : bb::launch_step(s->n, s->p, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
     }
     if (!ev.empty()) {
@@ -820,7 +806,8 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     }
     for (int32_t k = 0; k < (loop ? 0 : n); k++) {
         pp.c.action = actions + (int64_t)k * rows;
-        hipError_t e = ev.empty() ? launch_one_step(s, pp, st) : launch_one_step(s, pp, st, ev[2 * k], ev[2 * k + 1]);
+        hipError_t e = ev.empty() ? bb::launch_step(s->n, pp, st)
+                                  : bb::launch_step(s->n, pp, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
     }
     if (n > 0) {
@@ -1572,15 +1559,6 @@ int bb_diag_step_loop(int32_t v)
 {
     if (v < -1 || v > 2) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_loop: -1, 0, 1 or 2");
     g_step_loop_force = v;
-    return BB_OK;
-}
-
-// Diagnostic (not in the public header): the per-call step's kernel, k_step
-// (0) or the resident loop's kernel for one step (1), for the calls that follow.
-int bb_diag_step_kernel(int32_t v)
-{
-    if (v < 0 || v > 1) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_kernel: 0 or 1");
-    g_step_kernel = v;
     return BB_OK;
 }
 

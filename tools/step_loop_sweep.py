@@ -1,7 +1,6 @@
 """bb_step_n_staged per-step kernel time (events) across world counts, by
 kind (bb_diag_step_loop): 2 register-resident rollout launch with per-step
-state stores, 1 one k_step_loop launch, 0 one k_step launch per step, 3 one
-launch per step of the resident loop's kernel (bb_diag_step_kernel(1)).  With
+state stores, 1 one k_step_loop launch, 0 one k_step launch per step.  With
 --check every column and the written-back action rows of each kind are
 compared with kind 0's (same initial state, same staged rows).
 
@@ -41,10 +40,8 @@ def main():
                                                  num_agents=a.agents, per_world_rng=True)
                 c.step_n(7, random_actions=True)
                 acts = c.stage_random_actions(37, action_seed=9, step0=50)
-                L.bb_diag_step_loop(0 if kind == 3 else kind)
-                L.bb_diag_step_kernel(1 if kind == 3 else 0)
+                L.bb_diag_step_loop(kind)
                 c.step_n_staged(acts)
-                L.bb_diag_step_kernel(0)
                 torch.cuda.synchronize()
                 got = {n: t.clone() for n, t in c._views.items()}
                 got["staged"] = acts.clone()
@@ -58,8 +55,7 @@ def main():
             L.bb_diag_step_loop(-1)
         res = {}
         for kind in kinds:
-            L.bb_diag_step_loop(0 if kind == 3 else kind)
-            L.bb_diag_step_kernel(1 if kind == 3 else 0)
+            L.bb_diag_step_loop(kind)
             ts = []
             for r in range(a.reps):
                 acts = sim.stage_random_actions(a.steps, action_seed=5, step0=100 + r * a.steps)
@@ -67,7 +63,6 @@ def main():
                 del acts
             res[kind] = statistics.median(ts)
         L.bb_diag_step_loop(-1)
-        L.bb_diag_step_kernel(0)
         print(f"worlds {W:7d} x {a.agents}  " + "   ".join(f"kind {k} {res[k]:8.2f} us/step" for k in kinds),
               flush=True)
         del sim
