@@ -95,25 +95,6 @@ def cpu_executor_baseline(num_agents: int, seconds: float, threads: int):
             "sample": f"{w} worlds x {st} steps on {threads} threads, {num_agents} agents, threefry random actions"}
 
 
-STAGED_KERNEL = {0: "bb::k_step<%d>", 1: "bb::k_step_loop<%d>"}
-
-
-def staged_kernel(path: int, n_agents: int, worlds: int) -> str:
-    """The kernel bb_step_n_staged launches (bb_step_staged_path): 2 = the
-    register-resident loop (STORE = true instances), k_rollout_split<2> while
-    its 2-wave workgroups fit two per CU, k_rollout<2, 1> while the grid is at
-    most one wave per SIMD, else k_rollout<2, 2> (launch_rollout_t)."""
-    if path != 2:
-        return STAGED_KERNEL[path] % n_agents
-    if n_agents != 2:
-        return "bb::k_rollout_shared<%d, true, false>" % n_agents
-    import torch
-    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
-    waves = (worlds * n_agents + 63) // 64
-    return ("bb::k_rollout_split<2, true>" if waves <= 2 * cus
-            else "bb::k_rollout<2, %d, 1, true>" % (1 if waves <= 4 * cus else 2))
-
-
 def load_traffic(workload_key: str):
     """HBM bytes per step-kernel launch from the committed PMC passes
     (tools/traffic.py; FETCH_SIZE x2 + WRITE_SIZE), or None."""
@@ -327,6 +308,24 @@ def main():
     barrier()
     elapsed = max_over_ranks(elapsed)
 
+    # the drop-in path's own timed region: the same number of steps, each one
+    # launch of the kernel SimpleGridworldSimulator.step() issues (k_step,
+    # scripts/env.py:155 inside scripts/run.py:10-15's loop), reading its
+    # staged action rows; bit-identical results to the headline's launch
+    per_call_s = None
+    if on_gpu and not K and not args.policy:
+        del staged
+        staged = sim.stage_random_actions(args.steps, action_seed=args.seed, step0=args.warmup + args.steps)
+        with _lib.diag(step_loop=0):
+            sim.step_n_staged(staged[:1].clone())  # (untimed: the kernel's first launch)
+            barrier()
+            t0 = time.perf_counter()
+            run(staged)
+            sync()
+            per_call_s = time.perf_counter() - t0
+            barrier()
+        per_call_s = max_over_ranks(per_call_s)
+
     # kernel timing: the step kernel's own start/end (hipExtLaunchKernel
     # events on the launch stream) over the same workload, re-staged; at
     # least EVENT_MIN_LAUNCHES launches whatever --steps is, so the line's
@@ -485,8 +484,7 @@ def main():
             line = {"worlds": W2 * world_size, "worlds_per_gpu": W2, "n_gpus": world_size, "agents": n2,
                     "steps": steps2, "value": W2 * world_size * steps2 / wall2, "unit": "env-steps/s",
                     "ms_per_step": wall2 * 1e3 / steps2,
-                    "kernel": ((("bb::k_rollout<%d>" if n2 == 2 else "bb::k_rollout_shared<%d>") % n2) if fused2
-                               else staged_kernel(path2, n2, W2)),
+                    "kernel": _lib.kernel_name(sim2._h, 2 if K2 else 1, K2 or steps2),
                     "launches_timed": 1 if loop2 else launches, "kernel_avg_us": k2 * 1e6,
                     "kernel_us_per_step": k2 * 1e6 / (K2 or 1), "achieved": b2 / k2 / 1e9,
                     "frac": b2 / k2 / 1e9 / HBM_PEAK_GBS, "traffic": load_traffic(key),
@@ -536,8 +534,8 @@ def main():
                     "us_per_step": wall2 * 1e6 / (K2 * rollouts), "rollout_avg_us_events": ev * 1e3,
                     "path": {1: "k_rollout_policy (one launch per rollout)",
                              2: "k_rollout_ppo: the first policy pass, then K x (the step + the next policy "
-                                "pass), one launch (k_policy + one k_step_ppo per step with "
-                                "MADRONA_BB_PPO_STEP_LOOP=0)",
+                                "pass), one launch (k_policy + one k_step_ppo per step with the "
+                                "ppo_step_loop path override = 0)",
                              3: "k_policy + k_step per step"}.get(path, str(path)),
                     "roofline": {"bound": "hbm", "scope": "whole PPO step (policy pass + world step + records)",
                                  "algorithmic_bytes_per_step": step_bytes,
@@ -635,8 +633,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": ((("bb::k_rollout<%d>" if args.agents == 2 else "bb::k_rollout_shared<%d>") % args.agents)
-                       if (K and fused) else staged_kernel(staged_path if loop_main else 0, args.agents, W)),
+            "kernel": _lib.kernel_name(sim._h, 2 if K else (1 if loop_main else 0), K or ev_steps),
             "kernel_avg_us": avg_kernel_s * 1e6,
             "algorithmic_bytes_per_launch": bytes_per_launch,
         },
@@ -659,7 +656,8 @@ def main():
             out["roofline"]["state_reload_loop"] = {
                 "kernel": "bb::k_step_loop<%d>" % args.agents, "kernel_avg_us": reload_s * 1e6,
                 "achieved": b1 / reload_s / 1e9, "frac": b1 / reload_s / 1e9 / HBM_PEAK_GBS,
-                "what": "the same steps with every state column reloaded each step (MADRONA_BB_STEP_LOOP=1)"}
+                "what": "the same steps with every state column reloaded each step (k_step_loop, step_loop path "
+                        "override = 1)"}
     if not on_gpu:
         out["roofline"] = None
         out["config"]["parallelism"] += " (host executor, gloo)"
@@ -670,6 +668,20 @@ def main():
                                      "rollouts_timed": launches,
                                      "timing": "events around each bb_rollout_policy call (its K policy passes, "
                                                "K steps and the next-value pass)"}
+    if per_call_s is not None:
+        pc = {"value": total_worlds * args.steps / per_call_s, "unit": "env-steps/s",
+              "ms_per_step": per_call_s * 1e3 / args.steps, "kernel": "bb::k_step<%d>" % args.agents,
+              "what": "the per-call path: one k_step launch per step, the launch SimpleGridworldSimulator.step() "
+                      "makes (scripts/env.py:155, scripts/run.py:10-15's loop without Python), timed over the "
+                      "same number of steps as the headline; bit-identical outputs"}
+        if loop_main and one_launch_s is not None:
+            pc["kernel_avg_us"] = one_launch_s * 1e6
+            pc["frac"] = out["roofline"]["one_launch_per_step"]["frac"]
+        out["per_call_step"] = pc
+        out["headline"] = ("value = the staged steps as one launch (" + out["roofline"]["kernel"] + "); every step "
+                           "stores all its outputs as a per-call step does, but no consumer runs between steps: an "
+                           "upper bound of the per-call path, whose own rate is per_call_step.value (the drop-in "
+                           "path) and e2e.value (env.py's Python loop)") if loop_main else "one k_step launch per step"
     if e2e is not None:
         out["e2e"] = e2e
     out.update(extra)

@@ -130,6 +130,8 @@ def load():
         "bb_rollout_bytes_per_world_step": (i64, [i32]),
         "bb_rollout_state_bytes_per_world": (i64, [i32]),
         "bb_last_error": (ctypes.c_char_p, []),
+        "bb_diag_set": (ctypes.c_int, [i32, i32]),
+        "bb_diag_kernel_name": (ctypes.c_char_p, [vp, i32, i32]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)
@@ -137,6 +139,50 @@ def load():
         fn.argtypes = args
     _lib = L
     return L
+
+
+# Path overrides of the library (bb_launch.h DiagKey, set through the
+# diagnostic bb_diag_set; -1 restores the product's own rule).  Tests and A/B
+# timing only: the library reads no environment variable to pick a kernel.
+DIAG_KEYS = {
+    "step_loop": 0,                  # bb_step_n_staged's launch kind (BB_STAGED_*)
+    "rollout_split": 1,              # k_rollout_split: 0 never, 1 always
+    "rollout_minw": 2,               # k_rollout's register budget: 1 or 2 waves per SIMD
+    "rollout_shared_max_n": 3,       # the N >= 4 K-step rollout kernel up to this many agents
+    "ppo_pwaves": 4,                 # k_rollout_policy's policy waves: 2 or 4
+    "ppo_fused_max_worlds": 5,       # k_rollout_policy up to this many worlds
+    "ppo_step_fused_min_worlds": 6,  # the fused PPO step from this many worlds (0: never)
+    "ppo_step_loop": 7,              # 0: one k_step_ppo launch per step
+    "policy_wg": 8,                  # k_policy_wg: 0 never, 1 always
+}
+
+
+def diag_set(name: str, value: int) -> None:
+    check(load().bb_diag_set(DIAG_KEYS[name], int(value)), f"bb_diag_set({name}, {value})")
+
+
+class diag:
+    """Context manager: `with diag(step_loop=0): ...` sets path overrides for
+    the block and restores the product's rules (-1) after it."""
+
+    def __init__(self, **overrides):
+        self.overrides = overrides
+
+    def __enter__(self):
+        for k, v in self.overrides.items():
+            diag_set(k, v)
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.overrides:
+            diag_set(k, -1)
+        return False
+
+
+def kernel_name(sim_handle, what: int, n: int) -> str:
+    """The kernel a call launches (0 bb_step, 1 bb_step_n_staged of n steps,
+    2 bb_rollout of n steps), from the library's own selection rules."""
+    return load().bb_diag_kernel_name(sim_handle, int(what), int(n)).decode()
 
 
 def check(rc: int, what: str) -> None:

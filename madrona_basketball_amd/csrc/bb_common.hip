@@ -4,14 +4,10 @@
 #include <hip/hip_runtime.h>
 #include "bb_launch.h"
 #include "bb_rng.h"
-#include <cstdlib>
 
 namespace bb {
 
-int force_rollout_split = [] {
-    const char *e = std::getenv("MADRONA_BB_ROLLOUT_SPLIT");
-    return e && *e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
-}();
+int diag_override[DIAG_KEYS] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};
 
 // one lane = one (world, agent) action row (24 B); N compile-time so the
 // row -> (world, agent) split is a multiply, not a 64-bit division
@@ -394,19 +390,10 @@ bool step_records(int n)
 // beats per-step launches (65 536 worlds: 45.3 vs 62.7 us per step); from
 // N = 6 the row-source table sits beside the world instead (the register copy
 // spills), which costs occupancy: N = 10 396 vs 290 us per step
-// (profiles/r05/g_*, h_*).  MADRONA_BB_ROLLOUT_SHARED_MAX_N overrides it.
-static int rollout_shared_max_n()
-{
-    static const int v = [] {
-        const char *e = getenv("MADRONA_BB_ROLLOUT_SHARED_MAX_N");
-        return e && *e ? atoi(e) : 4;
-    }();
-    return v;
-}
-
+// (profiles/r05/g_*, h_*).  DIAG_ROLLOUT_SHARED_MAX_N overrides it (tests).
 bool fused_rollout_n(int n)
 {
-    if (n >= 4 && n > rollout_shared_max_n()) return false;
+    if (n >= 4 && n > diag_or(DIAG_ROLLOUT_SHARED_MAX_N, 4)) return false;
     switch (n) {
     case 2: return fused_rollout<2>();
     case 4: return fused_rollout<4>();
@@ -414,6 +401,18 @@ bool fused_rollout_n(int n)
     case 8: return fused_rollout<8>();
     case 10: return fused_rollout<10>();
     default: return false;
+    }
+}
+
+int rollout_kernel_n(int n, int64_t num_worlds)
+{
+    switch (n) {
+    case 2: return rollout_kernel_t<2>(num_worlds);
+    case 4: return rollout_kernel_t<4>(num_worlds);
+    case 6: return rollout_kernel_t<6>(num_worlds);
+    case 8: return rollout_kernel_t<8>(num_worlds);
+    case 10: return rollout_kernel_t<10>(num_worlds);
+    default: return RK_NONE;
     }
 }
 

@@ -17,8 +17,6 @@
 #include <functional>
 #include <memory>
 #include <mutex>
-#include <pthread.h>
-#include <sched.h>
 #include <string>
 #include <thread>
 #include <vector>
@@ -152,21 +150,10 @@ class HostPool {
 public:
     explicit HostPool(int n) : n_(n < 1 ? 1 : n)
     {
-        // BB_CPU_PIN=1: every share on a pool thread pinned to its own CPU of
-        // the process's affinity set, the caller only waiting.  Off by
-        // default: on 8 container cores (2 048 worlds per thread) 2 threads
-        // 3.36 -> 3.97 M env-steps/s and 8 threads 11.5 -> 11.8, but on the
-        // GPU box's 16-core share 46.9 M pinned against 52-61 M unpinned in
-        // earlier runs (profiles/r03/final_bench.log).
-        const char *pin = std::getenv("BB_CPU_PIN");
-        pinned_ = pin && *pin == '1' && n_ > 1;
-        cpu_set_t allowed;
-        CPU_ZERO(&allowed);
-        if (pinned_ && sched_getaffinity(0, sizeof(allowed), &allowed) == 0) {
-            for (int c = 0; c < CPU_SETSIZE; c++)
-                if (CPU_ISSET(c, &allowed)) cpus_.push_back(c);
-        }
-        for (int t = pinned_ ? 0 : 1; t < n_; t++) th_.emplace_back([this, t] { worker(t); });
+        // (threads pinned to CPUs measured slower on the GPU box's 16-core
+        // share: 46.9 M pinned against 52-61 M env-steps/s unpinned,
+        // profiles/r03/final_bench.log)
+        for (int t = 1; t < n_; t++) th_.emplace_back([this, t] { worker(t); });
     }
     ~HostPool()
     {
@@ -185,11 +172,11 @@ public:
         {
             std::lock_guard<std::mutex> g(m_);
             job_ = &f;
-            left_.store(pinned_ ? n_ : n_ - 1, std::memory_order_relaxed);
+            left_.store(n_ - 1, std::memory_order_relaxed);
             gen_.fetch_add(1, std::memory_order_release);
         }
         cv_.notify_all();
-        if (!pinned_) f(0);
+        f(0);
         // the others: spin, then sleep
         for (int i = 0; left_.load(std::memory_order_acquire) != 0; i++) {
             if (i > 4096) {
@@ -205,12 +192,6 @@ public:
 private:
     void worker(int t)
     {
-        if (pinned_ && !cpus_.empty()) {
-            cpu_set_t one;
-            CPU_ZERO(&one);
-            CPU_SET(cpus_[(size_t)t % cpus_.size()], &one);
-            (void)pthread_setaffinity_np(pthread_self(), sizeof(one), &one);
-        }
         uint64_t seen = 0;
         for (;;) {
             uint64_t g = gen_.load(std::memory_order_acquire);
@@ -238,8 +219,6 @@ private:
         }
     }
     const int n_;
-    bool pinned_ = false;
-    std::vector<int> cpus_;
     std::vector<std::thread> th_;
     std::mutex m_;
     std::condition_variable cv_, done_cv_;
@@ -695,54 +674,27 @@ int bb_fill_random_actions(bb_sim *s, int32_t *actions, int32_t n, uint32_t acti
 // k_rollout_split launch with RolloutArgs::store_state -- the state stays in
 // registers between steps and every step stores all of its columns, rows,
 // rewards, done flags and action write-backs where k_step does.
-// MADRONA_BB_STEP_LOOP = 0 / 1 / 2 forces one; default 2 (measured faster at
-// every size, bit-identical: 8 192 x 2 6.70 -> 4.93 us per step, 65 536
-// 19.30 -> 15.76, 262 144 61.5 -> 59.8; profiles/r05/an_sweep.txt,
-// ao_sweep.txt).
-static int g_step_loop_force = -1;  // bb_diag_step_loop: -1 by the environment, else the kind
+// Default 2 (measured faster at every size, bit-identical: 8 192 x 2 6.70 ->
+// 4.93 us per step, 65 536 19.30 -> 15.76, 262 144 61.5 -> 59.8;
+// profiles/r05/an_sweep.txt, ao_sweep.txt), at every agent count (the
+// shared-world loop: 65 536 x 4 64.4 -> 53.6 us per step, x 10 291.7 -> 246.0,
+// profiles/r05/aa_step_loop_n.txt); DIAG_STEP_LOOP forces a kind (tests, the
+// bench's per-launch objects).
 static int step_loop_kind()
 {
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_STEP_LOOP");
-        const int k = e && *e ? std::atoi(e) : 2;
-        return k < 0 || k > 2 ? 2 : k;
-    }();
-    return g_step_loop_force >= 0 ? g_step_loop_force : v;
-}
-
-// ... up to this many agents (MADRONA_BB_STEP_LOOP_MAX_N; default: every N --
-// the shared-world loop measured 64.4 -> 53.6 us per step at 65 536 x 4,
-// 291.7 -> 246.0 at 65 536 x 10, profiles/r05/aa_step_loop_n.txt).
-static int step_loop_max_n()
-{
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_STEP_LOOP_MAX_N");
-        return e && *e ? std::atoi(e) : 10;
-    }();
-    return v;
-}
-
-// ... the resident loop up to this many agents (MADRONA_BB_STEP_RESIDENT_MAX_N;
-// default 10: from N = 4 on k_rollout_shared's resident instances, taken while
-// the step stays in the Infinity Cache, bb::resident_staged)
-static int resident_max_n()
-{
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_STEP_RESIDENT_MAX_N");
-        return e && *e ? std::atoi(e) : 10;
-    }();
-    return v;
+    const int k = bb::diag_or(bb::DIAG_STEP_LOOP, 2);
+    return k > 2 ? 2 : k;
 }
 
 // The launch bb_step_n_staged makes for n steps (BB_STAGED_*; the host
-// executor: BB_STAGED_PER_STEP).
+// executor: BB_STAGED_PER_STEP).  The resident loop at N >= 4 is
+// k_rollout_shared's resident instance, taken while the step stays in the
+// Infinity Cache (bb::resident_staged).
 static int staged_path(const bb_sim *s, int32_t n)
 {
-    if (s->cfg.exec_mode != BB_EXEC_CUDA || n < 2 || s->n > step_loop_max_n()) return BB_STAGED_PER_STEP;
+    if (s->cfg.exec_mode != BB_EXEC_CUDA || n < 2) return BB_STAGED_PER_STEP;
     const int k = step_loop_kind();
-    if (k == 2)
-        return s->n <= resident_max_n() && bb::resident_staged_n(s->n, s->cfg.num_worlds) ? BB_STAGED_RESIDENT
-                                                                                          : BB_STAGED_LOOP;
+    if (k == 2) return bb::resident_staged_n(s->n, s->cfg.num_worlds) ? BB_STAGED_RESIDENT : BB_STAGED_LOOP;
     return k == 1 ? BB_STAGED_LOOP : BB_STAGED_PER_STEP;
 }
 
@@ -1022,86 +974,25 @@ bb::Params shard_params(const bb::Params &p, int N, int64_t w0, int64_t count)
 // K = 32, all records (profiles/r04/r_*, v_*, z_*): 32 768 worlds 41.0 ->
 // 35.4 us, 65 536 56.1 -> 50.1-51.3 (k_policy<1> halves 51.9-53.2,
 // k_policy_wg 54.7-55.5), 131 072 99.5 -> 92.5, 262 144 187.2 -> 176.4.
-// MADRONA_BB_PPO_SPLIT_MIN_WORLDS overrides it (0: never split).
-static int64_t ppo_split_min_worlds()
-{
-    static const int64_t v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_MIN_WORLDS");
-        return (int64_t)(e && *e ? std::atoll(e) : 32768);
-    }();
-    return v;
-}
-
 // The parts are independent worlds, so nothing orders them but the start:
-// part h's first policy pass waits for part h - 1's.  Re-aligning them every
-// step (an event per step) measured 54.5-55.7 vs 52.3-53.5 us per step
-// (profiles/r04/v_*); MADRONA_BB_PPO_SPLIT_SYNC=k re-aligns every k steps.
-static int ppo_split_sync_every()
-{
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_SYNC");
-        return e && *e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
-// The parts' policy kernel: k_policy<MT> (1, 2, 4; default 2), 0: launch_policy's
-// own choice for the part's rows (MADRONA_BB_POLICY_WG=1 then forces k_policy_wg)
-static int ppo_split_mt()
-{
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_MT");
-        return e && *e ? std::atoi(e) : 2;
-    }();
-    return v;
-}
-
-// (A/B) MADRONA_BB_PPO_REC_ONLY=0: the per-step loop's steps also write the
-// trainee's rows into the sim's obs (and the policy reads them there)
-static bool ppo_rec_only()
-{
-    static const bool v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_REC_ONLY");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-
-// World parts of the split loop (2 .. bb_sim::MAX_PARTS), MADRONA_BB_PPO_SPLIT_PARTS
-static int ppo_split_parts()
-{
-    static const int v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_SPLIT_PARTS");
-        const int k = e && *e ? std::atoi(e) : 2;
-        return k < 2 ? 2 : (k > bb_sim::MAX_PARTS ? bb_sim::MAX_PARTS : k);
-    }();
-    return v;
-}
+// part h's first policy pass waits for part h - 1's (re-aligning them every
+// step, an event per step, measured 54.5-55.7 vs 52.3-53.5 us per step,
+// profiles/r04/v_*).  The parts' policy kernel is k_policy<2> (276 registers:
+// a policy wave fits beside a step wave on one SIMD).
+constexpr int64_t PPO_SPLIT_MIN_WORLDS = 32768;
+constexpr int PPO_SPLIT_PARTS = 2;
+constexpr int PPO_SPLIT_MT = 2;
 
 // The fused PPO rollout (k_rollout_policy) runs one workgroup of 3 waves per
 // 32 worlds at one workgroup per CU (register-bound): used up to two waves of
 // workgroups -- measured 8 192 worlds 15.1 vs 27.6 us per step unfused,
 // 16 384: 29.7 vs 33.4, 65 536: 115 vs 64 (profiles/r03/g_ppo_fused_ab.txt).
-// MADRONA_BB_PPO_FUSED_MAX_WORLDS overrides the bound.
-static int64_t ppo_fused_max_worlds()
-{
-    static const int64_t v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_FUSED_MAX_WORLDS");
-        return (int64_t)(e && *e ? std::atoll(e) : 16384);
-    }();
-    return v;
-}
+// DIAG_PPO_FUSED_MAX_WORLDS overrides the bound (tests).
+static int64_t ppo_fused_max_worlds() { return bb::diag_or(bb::DIAG_PPO_FUSED_MAX_WORLDS, 16384); }
 
 // The fused step's rollout as one k_rollout_ppo launch (default) or as one
-// k_step_ppo launch per step (MADRONA_BB_PPO_STEP_LOOP=0; bit-identical).
-static bool ppo_step_loop()
-{
-    static const bool v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_STEP_LOOP");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    return v;
-}
+// k_step_ppo launch per step (DIAG_PPO_STEP_LOOP = 0; bit-identical, tests).
+static bool ppo_step_loop() { return bb::diag_or(bb::DIAG_PPO_STEP_LOOP, 1) != 0; }
 
 // PPO's loop with the trainee's policy pass fused behind the world step (its
 // rows read from LDS; k_rollout_ppo) from this many worlds on, wherever the
@@ -1109,15 +1000,8 @@ static bool ppo_step_loop()
 // measured 24 576 worlds 31.2 -> 20.0 us per step against the two-stream
 // split, while at 8 192 / 16 384 k_rollout_policy stays ahead (10.1 / 12.4 vs
 // 18.2 / 19.2; profiles/r05/k_small_ab.txt).
-// MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never).
-static int64_t ppo_step_fused_min_worlds()
-{
-    static const int64_t v = [] {
-        const char *e = std::getenv("MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS");
-        return (int64_t)(e && *e ? std::atoll(e) : 1);
-    }();
-    return v;
-}
+// DIAG_PPO_STEP_FUSED_MIN_WORLDS overrides it (0: never; tests).
+static int64_t ppo_step_fused_min_worlds() { return bb::diag_or(bb::DIAG_PPO_STEP_FUSED_MIN_WORLDS, 1); }
 
 // The implementation bb_rollout_policy takes (BB_PPO_PATH_*).
 static int32_t ppo_path(const bb_sim *s, bool opponent, uint32_t flags)
@@ -1218,48 +1102,13 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         r.obs_out = out->obs; r.act_out = out->actions; r.log_prob = out->log_prob; r.value = out->value;
         r.reward = out->reward; r.done = out->done; r.next_value = out->next_value;
         r.steps = n; r.trainee = trainee; r.stochastic = stochastic ? 1 : 0; r.seed = seed; r.step0 = step0;
-        uint64_t *ts = nullptr;
-        const char *tr = std::getenv("MADRONA_BB_PPO_TRACE");  // diagnostics: per-step clocks of workgroup 0
-        const int64_t groups = (W + 31) / 32;
-        const size_t TP = 24;  // PPO_TRACE_POINTS (bb_kernels.hip)
-        const size_t words = (size_t)n * TP + 2 * (size_t)groups;  // per-step clocks of workgroup 0, per-workgroup span
-        if (tr && *tr && hipMalloc(&ts, words * 8) == hipSuccess) r.diag_ts = ts;
         hipError_t e = bb::launch_rollout_policy(s->n, s->p, r, st);
         if (e != hipSuccess) return hip_fail(e, "launch fused PPO rollout kernel");
-        if (ts) {
-            std::vector<uint64_t> h(words);
-            if (hipMemcpyAsync(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-                hipStreamSynchronize(st) == hipSuccess) {
-                FILE *f = std::fopen(tr, "a");
-                if (f) {
-                    for (int32_t k = 0; k < n; k++) {
-                        std::fprintf(f, "%d", k);
-                        for (size_t i = 0; i < TP; i++) std::fprintf(f, " %llu", (unsigned long long)h[TP * k + i]);
-                        std::fprintf(f, "\n");
-                    }
-                    for (int64_t b = 0; b < groups; b++)
-                        std::fprintf(f, "wg %lld %llu %llu\n", (long long)b, (unsigned long long)h[(size_t)n * TP + 2 * b],
-                                     (unsigned long long)h[(size_t)n * TP + 2 * b + 1]);
-                    std::fclose(f);
-                }
-            }
-            (void)hipFree(ts);
-        }
     }
     const bool step_fused = path == BB_PPO_PATH_FUSED_STEP;
     if (step_fused) {
         // policy pass 0 on the sim's rows, then per step k one k_step_ppo:
         // step k, then policy pass k + 1 (or the value pass after the last step)
-        // (diagnostics: MADRONA_BB_PPO_STEP_DIAG skip bits, MADRONA_BB_PPO_STEP_TRACE
-        // a file that receives every launch's per-wave phase clocks)
-        static const uint32_t diag = [] {
-            const char *e = std::getenv("MADRONA_BB_PPO_STEP_DIAG");
-            return (uint32_t)(e && *e ? std::atoi(e) : 0);
-        }();
-        const char *trace = std::getenv("MADRONA_BB_PPO_STEP_TRACE");
-        const int64_t waves = (W + 31) / 32;
-        uint64_t *ts = nullptr;
-        if (trace && *trace && hipMalloc(&ts, (size_t)n * waves * bb::PPS_TRACE_POINTS * 8) != hipSuccess) ts = nullptr;
         // (the k_step_ppo launches need the policy pass of step 0 before them;
         // k_rollout_ppo runs it itself)
         const bool in_kernel = ppo_step_loop();
@@ -1273,8 +1122,6 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             a.act0 = out->actions;
             a.log_prob0 = out->log_prob;
             a.value0 = out->value;
-            a.diag = diag;
-            a.diag_ts = ts;
             a.w = policy_weights(w);
             a.trainee = trainee; a.stochastic = stochastic ? 1 : 0; a.seed = seed;
             a.step = step0 + 1u;
@@ -1291,8 +1138,6 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
         }
         for (int32_t k = 0; k < (ppo_step_loop() ? 0 : n) && e == hipSuccess; k++) {
             bb::PpoStepArgs a{};
-            a.diag = diag;
-            a.diag_ts = ts ? ts + (size_t)k * waves * bb::PPS_TRACE_POINTS : nullptr;
             a.w = policy_weights(w);
             a.trainee = trainee; a.stochastic = stochastic ? 1 : 0; a.seed = seed;
             a.step = step0 + (uint32_t)(k + 1);
@@ -1311,18 +1156,6 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 a.value = out->next_value;
             }
             e = bb::launch_step_ppo(s->n, s->p, a, st);
-        }
-        if (ts) {
-            std::vector<uint64_t> h((size_t)n * waves * bb::PPS_TRACE_POINTS);
-            if (e == hipSuccess && hipMemcpyAsync(h.data(), ts, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
-                hipStreamSynchronize(st) == hipSuccess) {
-                FILE *f = std::fopen(trace, "wb");
-                if (f) {
-                    std::fwrite(h.data(), 8, h.size(), f);
-                    std::fclose(f);
-                }
-            }
-            (void)hipFree(ts);
         }
         if (e != hipSuccess) return hip_fail(e, "bb_rollout_policy fused step launch");
     }
@@ -1345,20 +1178,19 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
             adv(a.done_out, 1);
         }
         a.key_row0 = (uint32_t)w0;
-        a.mt = ppo_split_mt();  // k_policy<2>: 276 registers, a policy wave fits beside a step wave on one SIMD
+        a.mt = PPO_SPLIT_MT;
         return a;
     };
     // the split needs at least 32 worlds (one policy tile) per part
-    const bool split = !fused && !step_fused && ppo_split_min_worlds() > 0 && W >= ppo_split_min_worlds() &&
-                       W >= 32 * (int64_t)ppo_split_parts();
+    const bool split = !fused && !step_fused && W >= PPO_SPLIT_MIN_WORLDS && W >= 32 * (int64_t)PPO_SPLIT_PARTS;
     // steps 0 .. n-2 write the trainee's rows into buffer.obs[k + 1] only (the
     // sim's copy of them is read by nobody before the last step rewrites
     // every row); the next policy pass reads them there.  Only the agent-lane
     // step kernel records (bb::step_records); elsewhere the policy pass keeps
     // the record and reads the sim's rows.
     const bool step_rec = bb::step_records(s->n);
-    const bool rec_only = out->obs != nullptr && ppo_rec_only() && step_rec;
-    const int parts = split ? ppo_split_parts() : 1;
+    const bool rec_only = out->obs != nullptr && step_rec;
+    const int parts = split ? PPO_SPLIT_PARTS : 1;
     constexpr int MP = bb_sim::MAX_PARTS;
     hipStream_t pst[MP] = {st, st, st, st};
     if (split) {
@@ -1427,8 +1259,7 @@ int bb_rollout_policy(bb_sim *s, const bb_policy_weights *w, const bb_policy_wei
                 if (split) o = part_pass(o, pw0[h], pcnt[h], sp[h]);
                 e = bb::launch_policy(o, pst[h]);
             }
-            if (e == hipSuccess && split && h + 1 < parts &&
-                (k == 0 || (ppo_split_sync_every() > 0 && k % ppo_split_sync_every() == 0))) {
+            if (e == hipSuccess && split && h + 1 < parts && k == 0) {
                 // part h + 1's policy pass k starts when part h's has finished:
                 // it then runs beside part h's step
                 e = hipEventRecord(s->aux_ev[1 + h], pst[h]);
@@ -1558,7 +1389,7 @@ int32_t bb_exec_mode(const bb_sim *s) { return s ? s->cfg.exec_mode : -1; }
 int bb_diag_step_loop(int32_t v)
 {
     if (v < -1 || v > 2) return fail(BB_ERR_INVALID_ARG, "bb_diag_step_loop: -1, 0, 1 or 2");
-    g_step_loop_force = v;
+    bb::diag_override[bb::DIAG_STEP_LOOP] = v;
     return BB_OK;
 }
 
@@ -1567,7 +1398,48 @@ int bb_diag_step_loop(int32_t v)
 int bb_diag_force_rollout_split(int32_t v)
 {
     if (v < -1 || v > 1) return fail(BB_ERR_INVALID_ARG, "bb_diag_force_rollout_split: -1, 0 or 1");
-    bb::force_rollout_split = v;
+    bb::diag_override[bb::DIAG_ROLLOUT_SPLIT] = v;
+    return BB_OK;
+}
+
+// Diagnostic (not in the public header): the kernel a call launches, as
+// rocprofv3 names it (without the parameter list) -- what = 0: bb_step; 1:
+// bb_step_n_staged of n steps; 2: bb_rollout of n steps.  From the same
+// selection rules the launchers use (bench.py labels its lines with it).
+const char *bb_diag_kernel_name(const bb_sim *s, int32_t what, int32_t n)
+{
+    static thread_local std::string name;
+    if (!s || s->cfg.exec_mode != BB_EXEC_CUDA) return "";
+    const std::string N = std::to_string(s->n);
+    const auto rollout = [&](bool store) -> std::string {
+        switch (bb::rollout_kernel_n(s->n, s->cfg.num_worlds)) {
+        case bb::RK_SPLIT: return "bb::k_rollout_split<" + N + (store ? ", true>" : ">");
+        case bb::RK_MINW1: return "bb::k_rollout<" + N + (store ? ", 1, 1, true>" : ", 1>");
+        case bb::RK_MINW2: return "bb::k_rollout<" + N + (store ? ", 2, 1, true>" : ", 2>");
+        case bb::RK_SHARED: return "bb::k_rollout_shared<" + N + (store ? ", true>" : ">");
+        default: return "bb::k_step<" + N + ">";
+        }
+    };
+    if (what == 1) {
+        const int path = staged_path(s, n);
+        name = path == BB_STAGED_RESIDENT ? rollout(true)
+             : path == BB_STAGED_LOOP     ? "bb::k_step_loop<" + N + ">"
+                                          : "bb::k_step<" + N + ">";
+    } else if (what == 2) {
+        name = bb::fused_rollout_n(s->n) ? rollout(false) : "bb::k_step<" + N + ">";
+    } else {
+        name = "bb::k_step<" + N + ">";
+    }
+    return name.c_str();
+}
+
+// Diagnostic (not in the public header): a path override of bb_launch.h's
+// DiagKey table for the calls that follow (-1: the product's own rule).  The
+// only way to change a launch choice: nothing is read from the environment.
+int bb_diag_set(int32_t key, int32_t value)
+{
+    if (key < 0 || key >= bb::DIAG_KEYS || value < -1) return fail(BB_ERR_INVALID_ARG, "bb_diag_set: key / value");
+    bb::diag_override[key] = value;
     return BB_OK;
 }
 

@@ -51,9 +51,6 @@ constexpr int WAVE = 64;
 #ifndef BB_LINES_AUX
 #define BB_LINES_AUX 2  // k_step, state beyond the Infinity Cache
 #endif
-#ifndef BB_RESIDENT_COL_AUX
-#define BB_RESIDENT_COL_AUX -1  // the resident staged loop's state columns (A/B)
-#endif
 #ifndef BB_ROLLOUT_AUX
 #define BB_ROLLOUT_AUX 2  // k_rollout: rows into a fresh K-step buffer
 #endif
@@ -715,9 +712,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
     // Everything loaded so far has arrived before the loop: no register
     // enters it with a load pending (which would make the compiler wait for
     // the vector-memory counter inside every step).
-#if !defined(BB_RO_NO_PREWAIT)
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
     for (int t = 0; t < r.steps; t++) {
         // Opaque per-step copies of the lane and world index: what derives
         // from them (column addresses, agent ids, the tile flush's per-piece
@@ -750,9 +745,7 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
             // (unconditional -- the last step re-reads its own rows -- so that
             // every path through the loop has the same loads in flight)
             load_words<6 * N>(t + 1 < r.steps ? act_t + rows * 6 : act_t, w_t, a_next);
-#if !defined(BB_RO_NO_SYS)
             step_world_pre_obs(s, c, ag);
-#endif
             // Retire the prefetch here, before this step's stores are issued:
             // waiting for it then waits only for what was issued before it
             // (the previous step's stores, drained during these systems).  At
@@ -769,8 +762,8 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
                 // into the sim's columns (r.reward / r.done here)
                 Params ps = p;
                 ps.c.action = act_t;
-                store_world_agent<N, BB_RESIDENT_COL_AUX>(v, ps, row, 0);
-                if (k == 0) store_world_shared<N, BB_RESIDENT_COL_AUX>(v, p, w_t);
+                store_world_agent<N>(v, ps, row, 0);
+                if (k == 0) store_world_shared<N>(v, p, w_t);
             } else {
                 r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
                 r.done[(int64_t)t * r.rd_step + row] = v.done[0];
@@ -787,12 +780,10 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
             }
         }
         __syncthreads();  // parked rows read before the tile is rewritten
-#if !defined(BB_RO_NO_OBS)
         // (the last step of a recorded rollout: the rows into the sim's tensor too)
         agent_lane_obs<N, MODE_FULL, T>(v, c, ib, share, k, lane_t, w0, w_t, active, tile,
                                         r.obs + (int64_t)t * r.obs_step,
                                         t + 1 == r.steps && r.obs_step != 0);
-#endif
         __syncthreads();  // the tile is rewritten by the next step
     }
     if (!STORE && active && r.steps > 0) {  // the simulator's own columns: state after the last step
@@ -893,8 +884,8 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
             if constexpr (STORE) {  // as in rollout_agent_lanes
                 Params ps = p;
                 ps.c.action = act_t;
-                store_world_agent<N, BB_RESIDENT_COL_AUX>(v, ps, row, 0);
-                if (k == 0) store_world_shared<N, BB_RESIDENT_COL_AUX>(v, p, w_t);
+                store_world_agent<N>(v, ps, row, 0);
+                if (k == 0) store_world_shared<N>(v, p, w_t);
             } else {
                 r.reward[(int64_t)t * r.rd_step + row] = v.rew[0];
                 r.done[(int64_t)t * r.rd_step + row] = v.done[0];
@@ -1045,32 +1036,6 @@ struct LdsRowSink {
     __device__ void finish() { while (idx & 3) put(0.f); }
 };
 
-// diagnostics (PolicyRolloutArgs::diag_ts, workgroup 0): per step k the clock
-// at 0 S starts the step (the actions are in LDS), 1 S's systems done, 20 S's
-// row sources (intrinsic blocks) done, 21 S's half-rows of pass 0 in X, 2 the
-// rows complete, 3 the first policy wave's actions done (for step k); the
-// first policy wave's pass for step k: 4 start (pass 0 of X in LDS), 5 (the
-// same), 6 layer-1 steps 0..15 issued, 7 the rows' second half in LDS, 8-12
-// at the five barriers of the layers (after each), 13-16 bucket pass stamps.
-constexpr int PPO_TRACE_POINTS = 24;
-__device__ __forceinline__ void ppo_trace(const PolicyRolloutArgs &r, int t, int point)
-{
-    if (r.diag_ts && blockIdx.x == 0) {
-        const uint64_t c = wall_clock64();
-        if (threadIdx.x % WAVE == 0) r.diag_ts[(int64_t)t * PPO_TRACE_POINTS + point] = c;
-    }
-}
-
-// diagnostics: every workgroup's sim-wave start (0) and end (1) clocks at
-// diag_ts[steps * PPO_TRACE_POINTS + 2 * workgroup + which]
-__device__ __forceinline__ void ppo_trace_wg(const PolicyRolloutArgs &r, int which)
-{
-    if (r.diag_ts) {
-        const uint64_t c = wall_clock64();
-        if (threadIdx.x == 0) r.diag_ts[(int64_t)r.steps * PPO_TRACE_POINTS + 2 * blockIdx.x + which] = c;
-    }
-}
-
 // The trainee's observation row in two hand-offs: pass P holds row floats i
 // with ((i >> 4) & 1) == P (for every lane group q of layer 1 the chain steps
 // j = 16P .. 16P + 15), written at their own positions of X.  With ROLE >= 0
@@ -1133,7 +1098,6 @@ template <int N, int PW>
 __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRolloutArgs &r, PpoLds<PW> &L, float *tile)
 {
     static_assert(N == 2, "the reference's 2-agent game");
-    ppo_trace_wg(r, 0);
     const int lane = threadIdx.x;
     const int64_t w0 = (int64_t)blockIdx.x * (WAVE / N);
     const int64_t w = w0 + lane / N;
@@ -1169,7 +1133,6 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         const LaneAgents<N, MODE_FULL> ag{k, &p};
         for (int b = 0; b < PpoCfg<PW>::LAYER_BARS; b++) lds_barrier();  // (the policy pass's own barriers)
         lds_barrier();  // the policy's actions are in LDS
-        ppo_trace(r, t, 0);
         int32_t ib = -1;
         bool share = false;
         if (active) {
@@ -1182,14 +1145,11 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             for (int i = 0; i < N; i++)
 #pragma unroll
                 for (int q = 0; q < 6; q++) s.act[i][q] = i == trainee ? a[q] : s.act[i][q];
-#if !defined(BB_PPO_NO_SYS)  // (diagnostic timing builds only: no systems)
             step_world_pre_obs(s, c, ag);
-#endif
             ib = inbounder_id(s);
             share = obs_sharable(s);
             agent_view(s, v, k);
         }
-        ppo_trace(r, t, 1);
         // the trainee's next observation row into X, in two hand-offs
         SharedObs<N> sh;
         lane_shared_obs(v, c, active, sh);
@@ -1205,12 +1165,10 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             sh.rdir[1][0] = l2 > 1e-6f ? to * rr : f3(0.f, 0.f, 0.f);
             sh.rlen[1][0] = bbm::sqrtf_(l2);
         }
-        ppo_trace(r, t, 20);
         float *xr = L.x[wl];
         lds_barrier();  // X is free: the policy waves have recorded buffer.obs[t] from it
         ppo_x_pass<0>(v, c, sh, active, is_trainee, split, fast, xr, ib);
         wave_sync();
-        ppo_trace(r, t, 21);
         lds_barrier();  // pass 0 of X: the policy waves start layer 1
         ppo_x_pass<1>(v, c, sh, active, is_trainee, split, fast, xr, ib);
         if (t + 1 == r.steps) {  // the sim's observation tensor: every row of the last step
@@ -1219,7 +1177,6 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
             obs_pass_wave<N, 1>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
         }
         wave_sync();
-        ppo_trace(r, t, 2);
         lds_barrier();  // X holds the observations after step t
         // reward (read by nothing on the way to the next actions) while the
         // policy waves run the network on X
@@ -1239,7 +1196,6 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         if (k == 0) store_world_shared(v, p, w_s);
     }
     for (int b = 0; b < PpoCfg<PW>::LAYER_BARS; b++) lds_barrier();  // (the next-value pass's barriers)
-    ppo_trace_wg(r, 1);
 }
 
 template <int PW>
@@ -1281,14 +1237,9 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
     if (r.stochastic) bucket_noise<RW>(noise, r.seed, r.step0, row0 + rh, W, lane);
     for (int t = 0; t <= r.steps; t++) {
         const bool final_pass = t == r.steps;  // agent.evaluate(obs_): value only
-        const bool tr = pw == 0 && !final_pass;
         lds_barrier();  // pass 0 of X: the rows' first half
-        if (tr) ppo_trace(r, t, 4);
-        if (tr) ppo_trace(r, t, 5);
         auto mid = [&] {
-            if (tr) ppo_trace(r, t, 6);
             lds_barrier();  // the rows' second half
-            if (tr) ppo_trace(r, t, 7);
         };
         float (*lt)[33];
         if constexpr (PW == 4) {
@@ -1300,19 +1251,16 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             policy_layers1_split(&L.x[r0 + c][0], R, L.norm, L.ptile[m], c, q, mid);
             lt = L.ptile[m];
         }
-        if (tr) ppo_trace(r, t, 12);
         a.step = r.step0 + (uint32_t)t;
         if (!final_pass) {
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
-            uint64_t *bts = (tr && r.diag_ts && blockIdx.x == 0) ? r.diag_ts + (int64_t)t * PPO_TRACE_POINTS + 13 : nullptr;
             if (r.stochastic)
-                bucket_pass_spread<RW, true>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise, bts);
+                bucket_pass_spread<RW, true>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise);
             else
-                bucket_pass_spread<RW, false>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr, bts);
+                bucket_pass_spread<RW, false>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr);
             pol_wave_sync();
-            if (pw == 0) ppo_trace(r, t, 3);
             lds_barrier();  // actions in LDS
             // while the sim wave steps: buffer.obs[t] = X (this wave's rows),
             // then the next step's sampling uniforms
@@ -1522,24 +1470,10 @@ __device__ __forceinline__ void ppo_emit_pass(const World<2> &v, const Ctx &c, c
     }
 }
 
-// diagnostics (PpoStepArgs::diag_ts): the wave's clock at 0 start, 1 state
-// loaded, 2 systems done, 3 state stores issued, 4 pass 0 in the tile, 5 pass 0
-// MFMAs and stores issued, 6 pass 1 in the tile, 7 pass 1 issued, 8 layers
-// done, 9 bucket pass done, 10 the wave's stores retired
-__device__ __forceinline__ void pps_trace(const PpoStepArgs &a, int64_t gw, int point, bool wait_mem = false)
-{
-    if (a.diag_ts) {
-        if (wait_mem) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint64_t t = wall_clock64();
-        if ((threadIdx.x & 63) == 0) a.diag_ts[gw * PPS_TRACE_POINTS + point] = t;
-    }
-}
-
 // Step k of a k_rollout_ppo launch: a0 holds step 0's outputs (reward /
 // done [k], buffer.obs / actions / log_probs / values [k + 1]); the last step
 // writes next_value (a0.value_last) and no buffer entries of step k + 1.
-__device__ __forceinline__ PpoStepArgs ppo_loop_args(const PpoStepArgs &a0, int32_t k, int32_t steps, int64_t W,
-                                                     int64_t waves)
+__device__ __forceinline__ PpoStepArgs ppo_loop_args(const PpoStepArgs &a0, int32_t k, int32_t steps, int64_t W)
 {
     PpoStepArgs a = a0;
     const int64_t o = (int64_t)k * W;
@@ -1560,7 +1494,6 @@ __device__ __forceinline__ PpoStepArgs ppo_loop_args(const PpoStepArgs &a0, int3
         if (a.log_prob) a.log_prob += o;
         if (a.value) a.value += o;
     }
-    if (a.diag_ts) a.diag_ts += (int64_t)k * waves * PPS_TRACE_POINTS;
     return a;
 }
 
@@ -1579,11 +1512,9 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     const int trainee = a.trainee;
     const LaneAgents<N, MODE_FULL> ag{k, &p};
 
-    const int64_t gw = (int64_t)blk * WPG + wave;
     World<N> s;
     Ctx c = make_ctx(p, w, k == 0);
     World<N> v;
-    pps_trace(a, gw, 0);
     if (active) {
         load_world(s, p, w);
         {
@@ -1600,11 +1531,9 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     // off the bucket pass's chain
     BucketNoise<32> noise;
     if (!LAST && a.stochastic) bucket_noise<32>(noise, a.seed, a.step, w0, p.num_worlds, lane);
-    pps_trace(a, gw, 1, true);
     // the workgroup's copy of the network (read after the barrier below)
     if (!LOOP) policy_weights_to_lds(S.wt, a.w, (int)threadIdx.x, WPG * WAVE);
     if (active) step_world_pre_obs(s, c, ag);
-    pps_trace(a, gw, 2);
     if (active) {
         agent_view(s, v, k);
         sys_reward_agent(v, 0, AGENT0_ID + k);
@@ -1620,16 +1549,14 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
             a.done[w] = v.done[0];
         }
     }
-    pps_trace(a, gw, 3);
     const int32_t ib = active ? inbounder_id(s) : -1;
     const bool share = active && obs_sharable(s);
     SharedObs<N> sh;
     lane_shared_obs(v, c, active, sh);
     const bool fast = active && canonical_slots(v, 0);
     const uint64_t live = __ballot(active);
-    const uint32_t diag = a.diag;  // (0 outside timing diagnostics)
     char *obs = (char *)(p.c.obs + w0 * N * (int64_t)obs_width(N));                // wave-uniform
-    char *rec = (!LAST && a.obs_rec && !(diag & 8u)) ? (char *)(a.obs_rec + w0 * (int64_t)POL_IN) : nullptr;
+    char *rec = (!LAST && a.obs_rec) ? (char *)(a.obs_rec + w0 * (int64_t)POL_IN) : nullptr;
     const int pl = lane & 15, pq = lane >> 4;
     f32x4 acc[2][2];
 #pragma unroll
@@ -1638,36 +1565,24 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
     ppo_emit_pass<0>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
     if (!LOOP) lds_barrier();  // the pass's rows, and the workgroup's weights, are in LDS
     else wave_sync();
-    pps_trace(a, gw, 4);
-    if (!(diag & 4u)) ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
+    ppo_layer1_pass<0>(tile, S.wt, acc, trainee, pl, pq);
     ppo_flush_pass<0, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
-    pps_trace(a, gw, 5);
     ppo_emit_pass<1>(v, c, sh, active, fast, share, tile + lane * PPS_RS, ib);
     wave_sync();
-    pps_trace(a, gw, 6);
-    if (!(diag & 4u)) ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
+    ppo_layer1_pass<1>(tile, S.wt, acc, trainee, pl, pq);
     ppo_flush_pass<1, LAST>(tile, obs, rec, live, trainee, lane);
     wave_sync();
-    pps_trace(a, gw, 7);
     if (LAST && !a.value) return;  // (wave-uniform; no barrier follows)
     // LayerNorm 1, layer 2, heads (the tile's first 32 x 33 floats), then the
     // bucket pass (its exchange right behind them)
     float (*lt)[33] = (float (*)[33])tile;
-    if (!(diag & 2u)) {
 #pragma unroll
-        for (int mt = 0; mt < 2; mt++)
-            ln_relu_to_tile(acc[mt][0], acc[mt][1], S.wt.cst[0][pl], S.wt.cst[0][pl + 16], S.wt.cst[1][pl],
-                            S.wt.cst[1][pl + 16], S.wt.cst[2][pl], S.wt.cst[2][pl + 16], lt + 16 * mt, pl, pq);
-        pol_wave_sync();
-        policy_tail_lds2(S.wt, lt, pl, pq);
-    }
-    pps_trace(a, gw, 8);
-    if (diag & 1u) {
-        pps_trace(a, gw, 9);
-        pps_trace(a, gw, 10, true);
-        return;
-    }
+    for (int mt = 0; mt < 2; mt++)
+        ln_relu_to_tile(acc[mt][0], acc[mt][1], S.wt.cst[0][pl], S.wt.cst[0][pl + 16], S.wt.cst[1][pl],
+                        S.wt.cst[1][pl + 16], S.wt.cst[2][pl], S.wt.cst[2][pl + 16], lt + 16 * mt, pl, pq);
+    pol_wave_sync();
+    policy_tail_lds2(S.wt, lt, pl, pq);
     if constexpr (LAST) {
         if (a.value && lane < 32 && w0 + lane < p.num_worlds) a.value[w0 + lane] = lt[lane][POL_LOGITS];
     } else {
@@ -1685,8 +1600,6 @@ __device__ __forceinline__ void ppo_step_wave(const Params &p, const PpoStepArgs
         if (a.stochastic) bucket_pass_spread<32, true, 1>(pa, lt, w0, lane, bl, nullptr, &noise);
         else bucket_pass_spread<32, true, 0>(pa, lt, w0, lane, bl, nullptr, &noise);
     }
-    pps_trace(a, gw, 9);
-    pps_trace(a, gw, 10, true);
 }
 
 // The policy pass of step 0 inside k_rollout_ppo (what a k_policy launch on
@@ -1797,7 +1710,7 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void k_rollout_ppo(const Params p, c
             // step 0 reads the action column the pass wrote
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         }
-        const int64_t W = p.num_worlds, waves = (W + WAVE / 2 - 1) / (WAVE / 2);
+        const int64_t W = p.num_worlds;
         for (int32_t k = 0; k < steps; k++) {
             // opaque per-step copies of the indices: nothing derived from them
             // (column addresses, the world's keys) is computed before the loop
@@ -1805,7 +1718,7 @@ __global__ __launch_bounds__(WAVE * WPG, 2) void k_rollout_ppo(const Params p, c
             int32_t k_t = k, blk_t = (int)blockIdx.x, wave_t = wave, lane_t = lane;
             __asm__ volatile("" : "+s"(k_t), "+s"(blk_t), "+s"(wave_t));
             __asm__ volatile("" : "+v"(lane_t));
-            const PpoStepArgs a = ppo_loop_args(a0, k_t, steps, W, waves);
+            const PpoStepArgs a = ppo_loop_args(a0, k_t, steps, W);
             if (k_t + 1 < steps) ppo_step_wave<WPG, false, true>(p, a, S, blk_t, wave_t, lane_t);
             else ppo_step_wave<WPG, true, true>(p, a, S, blk_t, wave_t, lane_t);
             // this step's state / action stores before the next step's loads
@@ -2356,16 +2269,17 @@ struct SharedRollout {
 };
 
 // STORE: bb_step_n_staged's resident loop (RolloutArgs::store_state) -- every
-// step stores the state columns with k_step_shared's cache policies (BEYOND:
-// the step's bytes exceed the Infinity Cache), rows into the sim's tensor.
-template <int N, class SM, bool STORE = false, bool BEYOND = false>
+// step stores the state columns with k_step_shared's cache policies (taken
+// only while the step's bytes fit the Infinity Cache, bb::resident_staged),
+// rows into the sim's tensor.
+template <int N, class SM, bool STORE = false>
 __device__ __forceinline__ void rollout_shared_world(const Params &p, const RolloutArgs &r, SM &sm)
 {
     using SR = SharedRollout<N>;
     constexpr int WPW = SM::WPW, OW = obs_width(N);
     // rows into a fresh [K][W][N][OBSW] buffer, or (STORE) as the step's
-    constexpr int AUX = !STORE ? BB_ROLLOUT_AUX : (BEYOND ? BB_SHARED_BEYOND_AUX : BB_SHARED_AUX);
-    constexpr int CAUX = BEYOND ? BB_SHARED_BEYOND_COL_AUX : BB_SHARED_AUX;
+    constexpr int AUX = !STORE ? BB_ROLLOUT_AUX : BB_SHARED_AUX;
+    constexpr int CAUX = BB_SHARED_AUX;
     const int lane = threadIdx.x;
     const bool lane_used = lane < WPW * N;
     const int slot = lane_used ? lane / N : WPW - 1;
@@ -2487,14 +2401,14 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
     }
 }
 
-template <int N, bool STORE = false, bool BEYOND = false>
+template <int N, bool STORE = false>
 __global__ __launch_bounds__(WAVE, 2) void k_rollout_shared(const Params p, const RolloutArgs r)
 {
     if constexpr (SharedRollout<N>::value) {
         __shared__ typename SharedRollout<N>::Lds sm;
         const uint4 *g = (const uint4 *)&PIECE_CODE<N>;
         for (int i = (int)threadIdx.x; i < obs_width(N) / 4; i += WAVE) sm.code[i] = g[i];
-        rollout_shared_world<N, typename SharedRollout<N>::Lds, STORE, BEYOND>(p, r, sm);
+        rollout_shared_world<N, typename SharedRollout<N>::Lds, STORE>(p, r, sm);
     }
 }
 
@@ -2564,23 +2478,6 @@ constexpr int tile_floats()
     return Lanes<N>::LPW == N ? StepTile<N, LINES>::FLOATS : ObsTile<N>::FLOATS;
 }
 
-// Start skew (timing experiment, off by default): wave group blockIdx % G
-// sleeps g * S s_sleep units before loading, so that groups sharing a SIMD
-// alternate between memory and compute phases instead of running in step.
-#ifndef BB_SKEW_G
-#define BB_SKEW_G 1
-#endif
-#ifndef BB_SKEW_S
-#define BB_SKEW_S 32
-#endif
-__device__ __forceinline__ void start_skew()
-{
-    if constexpr (BB_SKEW_G > 1) {
-        const int g = (int)(blockIdx.x % BB_SKEW_G);
-        for (int i = 0; i < g; i++) __builtin_amdgcn_s_sleep(BB_SKEW_S);
-    }
-}
-
 #ifndef BB_STEP_MINW
 #define BB_STEP_MINW 2  // waves per SIMD the register budget is sized for
 #endif
@@ -2591,7 +2488,6 @@ template <int N, int MODE, bool LINES = false, bool REC = false>
 __global__ __launch_bounds__(WAVE, BB_STEP_MINW) void k_step(const Params p)
 {
     __shared__ float4 tile4[tile_floats<N, LINES>() / 4];
-    start_skew();
     if constexpr (Lanes<N>::SHARED) {
         __shared__ SharedLds<N> sm;
         if constexpr (BB_OBS_PIECES && MODE != MODE_DIRECT_OBS && !SharedTiled<N>::value) {
@@ -2681,22 +2577,14 @@ __global__ __launch_bounds__(256) void k_init(const Params p)
 // comfortably in the 256 MiB Infinity Cache (see StepTile).
 constexpr int64_t LINES_MIN_BYTES = 192ll << 20;
 // N >= 4: the rows and columns are stored non-temporally once a step's bytes
-// exceed this (default 384 MiB; MADRONA_BB_NT_MIN_MB overrides it for A/B
-// timing).  Measured at 65 536 worlds: N = 4 (266 MB per step) 69.6 us plain
-// vs 73.9 nt; N = 10 (1.28 GB) 343 vs 323.
-inline int64_t shared_beyond_bytes()
-{
-    static const int64_t v = [] {
-        const char *e = getenv("MADRONA_BB_NT_MIN_MB");
-        return (int64_t)(e && *e ? atoll(e) : 384) << 20;
-    }();
-    return v;
-}
+// exceed this.  Measured at 65 536 worlds: N = 4 (266 MB per step) 69.6 us
+// plain vs 73.9 nt; N = 10 (1.28 GB) 343 vs 323.
+constexpr int64_t SHARED_BEYOND_BYTES = 384ll << 20;
 template <int N>
 bool step_lines(int64_t num_worlds)
 {
     const int64_t per_world = (int64_t)N * (obs_width(N) * 4 + 240) + 160;  // rows + state columns
-    if constexpr (Lanes<N>::SHARED) return num_worlds * per_world > shared_beyond_bytes();
+    if constexpr (Lanes<N>::SHARED) return num_worlds * per_world > SHARED_BEYOND_BYTES;
     return Lanes<N>::LPW == N && num_worlds * per_world > LINES_MIN_BYTES;
 }
 
@@ -2712,16 +2600,9 @@ static unsigned device_cus()
     return v;
 }
 
-// k_step_loop's workgroup size for a grid of `waves` (MADRONA_BB_STEP_LOOP_G
-// = 1 / 2 / 4 forces it; read once per process).
+// k_step_loop's workgroup size for a grid of `waves`.
 static int step_loop_group(int64_t waves)
 {
-    static const int forced = [] {
-        const char *e = getenv("MADRONA_BB_STEP_LOOP_G");
-        const int v = e && *e ? atoi(e) : 0;
-        return v == 1 || v == 2 || v == 4 ? v : 0;
-    }();
-    if (forced) return forced;
     // (49 152 worlds = 1.5 waves per SIMD: 4-wave workgroups leave half the CUs
     // with one workgroup and half with two, 18.1 us per step; 2-wave ones
     // spread evenly, 15.6)
@@ -2804,68 +2685,81 @@ hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev
 }
 
 // The whole-register-file rollout while the grid fits one wave per SIMD (every
-// CU of the device, 4 SIMDs each); env MADRONA_BB_ROLLOUT_MINW=1/2 forces it
-// (read once per process).
+// CU of the device, 4 SIMDs each); DIAG_ROLLOUT_MINW = 1 / 2 forces it (tests).
 static bool rollout_minw1(unsigned waves)
 {
-    static const int forced = [] {
-        const char *e = getenv("MADRONA_BB_ROLLOUT_MINW");
-        return e && *e ? atoi(e) : 0;
-    }();
+    const int forced = diag_or(DIAG_ROLLOUT_MINW, 0);
     if (forced) return forced == 1;
     return waves <= 4u * device_cus();
 }
 
 // k_rollout_split while its workgroups (2 waves) fit one wave per SIMD: at
-// most 2 per CU.  force_rollout_split (bb_common.hip: MADRONA_BB_ROLLOUT_SPLIT
-// at load, bb_diag_force_rollout_split at run time) forces it off / on (A/B,
-// tests).
+// most 2 per CU.  DIAG_ROLLOUT_SPLIT forces it off / on (tests).
 #ifndef BB_ROLLOUT_SPLIT
 #define BB_ROLLOUT_SPLIT 1
 #endif
 static bool rollout_split(unsigned groups)
 {
-    const int forced = force_rollout_split;
+    const int forced = diag_or(DIAG_ROLLOUT_SPLIT, -1);
     if (forced >= 0) return forced != 0;
     return BB_ROLLOUT_SPLIT != 0 && groups <= 2u * device_cus();
+}
+
+// The K-step rollout kernel a grid of num_worlds takes (RolloutKernel); the
+// launcher and the name query (bench.py's kernel names) use this one rule.
+template <int N>
+int rollout_kernel_t(int64_t num_worlds)
+{
+    if constexpr (SharedRollout<N>::value) {
+        return RK_SHARED;
+    } else if constexpr (!FusedRollout<N>::value) {
+        return RK_NONE;
+    } else {
+        const unsigned grid = (unsigned)((num_worlds + Lanes<N>::WPB - 1) / Lanes<N>::WPB);
+        return rollout_split(grid) ? RK_SPLIT : rollout_minw1(grid) ? RK_MINW1 : RK_MINW2;
+    }
 }
 
 template <int N>
 hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1)
 {
+    constexpr int WPB = Lanes<N>::WPB;
+    const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
+    if (r.store_state && (r.reward != p.c.reward || r.done != p.c.done || r.rd_step != 0))
+        return hipErrorInvalidValue;  // the resident loop stores reward / done with the state
+    const int kind = rollout_kernel_t<N>(p.num_worlds);
     if constexpr (SharedRollout<N>::value) {
-        constexpr int WPB = Lanes<N>::WPB;
-        const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-        if (r.store_state) {  // bb_step_n_staged's resident loop
-            if (r.reward != p.c.reward || r.done != p.c.done || r.rd_step != 0) return hipErrorInvalidValue;
-            if (step_lines<N>(p.num_worlds))
-                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N, true, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
-            else
-                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N, true, false>), grid, block, 0, s, ev0, ev1, 0, p, r);
-        } else {
+        // (the resident instance only while the step fits the Infinity Cache,
+        // bb::resident_staged: beyond it the reloading loop is faster)
+        if (r.store_state && step_lines<N>(p.num_worlds)) return hipErrorNotSupported;
+        if (r.store_state)
+            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
+        else
             hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_shared<N>), grid, block, 0, s, ev0, ev1, 0, p, r);
-        }
         return hipGetLastError();
     } else if constexpr (!FusedRollout<N>::value) {
         return hipErrorNotSupported;
     } else {
-        constexpr int WPB = Lanes<N>::WPB;
-        const dim3 grid((unsigned)((p.num_worlds + WPB - 1) / WPB)), block(WAVE);
-        const bool split = rollout_split(grid.x), minw1 = rollout_minw1(grid.x);
-        if (r.store_state) {  // bb_step_n_staged's resident loop
-            if (r.reward != p.c.reward || r.done != p.c.done || r.rd_step != 0) return hipErrorInvalidValue;
-            if (split)
+        switch (kind) {
+        case RK_SPLIT:
+            if (r.store_state)
                 hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N, true>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
-            else if (minw1)
+            else
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
+            break;
+        case RK_MINW1:
+            if (r.store_state)
                 hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1, 1, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
             else
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1>), grid, block, 0, s, ev0, ev1, 0, p, r);
+            break;
+        default:
+            if (r.store_state)
                 hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2, 1, true>), grid, block, 0, s, ev0, ev1, 0, p, r);
-        } else if (split)
-            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_split<N>), grid, dim3(2 * WAVE), 0, s, ev0, ev1, 0, p, r);
-        else if (minw1)
-            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 1>), grid, block, 0, s, ev0, ev1, 0, p, r);
-        else
-            hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2>), grid, block, 0, s, ev0, ev1, 0, p, r);
+            else
+                hipExtLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout<N, 2>), grid, block, 0, s, ev0, ev1, 0, p, r);
+            break;
+        }
         return hipGetLastError();
     }
 }
@@ -2878,15 +2772,11 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
     } else {
         // 4 policy waves while the grid is at most one workgroup per CU (8 192
         // worlds: 9.66 -> 9.48 us per step, profiles/r05/ad_pw_ab.txt), 2 above
-        // (16 384: 12.1 vs 18.2); MADRONA_BB_PPO_PWAVES = 2 / 4 forces it.
+        // (16 384: 12.1 vs 18.2); DIAG_PPO_PWAVES = 2 / 4 forces it (tests).
         // (3 waves: each its own SIMD; 5 waves share them -- the 256-register budget)
         const dim3 grid((unsigned)((p.num_worlds + 31) / 32));
-        static const int forced = [] {
-            const char *e = getenv("MADRONA_BB_PPO_PWAVES");
-            const int v = e && *e ? atoi(e) : 0;
-            return v == 2 || v == 4 ? v : 0;
-        }();
-        const int pw = forced ? forced : (grid.x <= device_cus() ? 4 : 2);
+        const int forced = diag_or(DIAG_PPO_PWAVES, 0);
+        const int pw = forced == 2 || forced == 4 ? forced : (grid.x <= device_cus() ? 4 : 2);
         if (pw == 4)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2, 4>), grid, dim3(WAVE * 5), 0, s, p, r);
         else if (grid.x <= device_cus())
@@ -2945,6 +2835,7 @@ template hipError_t launch_step_t<BB_N>(const Params &, int, hipStream_t, hipEve
 template hipError_t launch_step_loop_t<BB_N>(const Params &, int32_t *, int32_t, hipStream_t, hipEvent_t, hipEvent_t);
 template hipError_t launch_init_t<BB_N>(const Params &, hipStream_t);
 template hipError_t launch_rollout_t<BB_N>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t);
+template int rollout_kernel_t<BB_N>(int64_t);
 template hipError_t launch_rollout_policy_t<BB_N>(const Params &, const PolicyRolloutArgs &, hipStream_t);
 template <> bool fused_rollout<BB_N>() { return FusedRollout<BB_N>::value || SharedRollout<BB_N>::value; }
 template <> bool step_records_t<BB_N>() { return BB_N == 2 && Lanes<BB_N>::LPW == BB_N && !Lanes<BB_N>::SHARED; }

@@ -51,7 +51,6 @@ struct PolicyRolloutArgs {
     float *next_value;    // [W]
     int32_t steps, trainee, stochastic;
     uint32_t seed, step0;
-    uint64_t *diag_ts;    // diagnostics only: per-step phase clocks of workgroup 0 ([steps][4])
 };
 
 // One step of PPO's rollout loop with the policy fused behind it
@@ -79,14 +78,7 @@ struct PpoStepArgs {
     float *obs0;
     int32_t *act0;
     float *log_prob0, *value0;
-    // diagnostics only (timing attribution; the outputs are then wrong):
-    // diag bit 0 no bucket pass, 1 no LayerNorm-1 / layer 2 / heads, 2 no
-    // layer-1 MFMAs, 3 no buffer.obs stores; diag_ts: PPS_TRACE_POINTS clocks
-    // per wave
-    uint32_t diag;
-    uint64_t *diag_ts;
 };
-constexpr int PPS_TRACE_POINTS = 12;
 // N = 2 only (hipErrorNotSupported otherwise)
 hipError_t launch_step_ppo(int n, const Params &p, const PpoStepArgs &a, hipStream_t s);
 // The `steps` steps of a rollout in one launch (k_rollout_ppo<2>): `a` holds
@@ -104,9 +96,27 @@ struct RecordArgs {
 int32_t record_words(int n);
 RecordArgs record_args(const Params &p, int n);
 
-// k_rollout_split choice: -1 by grid size, 0 never, 1 always (diagnostics and
-// tests; bb_common.hip, bb_diag_force_rollout_split).
-extern int force_rollout_split;
+// Path overrides, for tests and A/B timing only: set through the C ABI's
+// bb_diag_set (not in the public header), never read from the environment.
+// -1 (the initial value) = the product's own rule for that choice.
+enum DiagKey : int {
+    DIAG_STEP_LOOP = 0,                  // bb_step_n_staged's launch: BB_STAGED_* (0 per step, 1 k_step_loop, 2 resident)
+    DIAG_ROLLOUT_SPLIT = 1,              // k_rollout_split: 0 never, 1 always (else while its grid fits 2 per CU)
+    DIAG_ROLLOUT_MINW = 2,               // k_rollout's register budget: 1 or 2 waves per SIMD
+    DIAG_ROLLOUT_SHARED_MAX_N = 3,       // the N >= 4 K-step rollout kernel up to this many agents (default 4)
+    DIAG_PPO_PWAVES = 4,                 // k_rollout_policy's policy waves: 2 or 4
+    DIAG_PPO_FUSED_MAX_WORLDS = 5,       // k_rollout_policy up to this many worlds (default 16 384)
+    DIAG_PPO_STEP_FUSED_MIN_WORLDS = 6,  // the fused PPO step from this many worlds (default 1; 0 never)
+    DIAG_PPO_STEP_LOOP = 7,              // 0: one k_step_ppo launch per step instead of one k_rollout_ppo
+    DIAG_POLICY_WG = 8,                  // k_policy_wg: 0 never, 1 always (else from 98 304 rows)
+    DIAG_KEYS = 9
+};
+extern int diag_override[DIAG_KEYS];
+inline int diag_or(int key, int dflt)
+{
+    const int v = diag_override[key];
+    return v >= 0 ? v : dflt;
+}
 
 template <int N> hipError_t launch_step_t(const Params &p, int mode, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1);
 template <int N> hipError_t launch_init_t(const Params &p, hipStream_t s);
@@ -118,6 +128,16 @@ template <int N> int step_grid(int64_t num_worlds);  // k_step workgroups (= wav
 template <int N> hipError_t launch_rollout_t(const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0,
                                              hipEvent_t ev1);
 template <int N> bool fused_rollout();  // k_rollout<N> exists (else: one k_step launch per step)
+// The K-step rollout kernel family a grid takes (launch_rollout_t; its
+// RolloutArgs::store_state instances for the resident loop).
+enum RolloutKernel : int {
+    RK_NONE = -1,   // no fused rollout: one k_step launch per step
+    RK_SPLIT = 0,   // k_rollout_split<N> (sim wave + row wave per 32 worlds)
+    RK_MINW1 = 1,   // k_rollout<N, 1>: the whole register file, at most one wave per SIMD
+    RK_MINW2 = 2,   // k_rollout<N, 2>
+    RK_SHARED = 3,  // k_rollout_shared<N> (N >= 4, the world in LDS)
+};
+template <int N> int rollout_kernel_t(int64_t num_worlds);
 // bb_step_n_staged's register-resident loop (RolloutArgs::store_state) is taken
 template <int N> bool resident_staged(int64_t num_worlds);
 template <int N> bool step_records_t();  // k_step<N> honours Params::rec_obs
@@ -129,6 +149,7 @@ template <int N> hipError_t launch_rollout_policy_t(const Params &p, const Polic
     extern template hipError_t launch_step_loop_t<n>(const Params &, int32_t *, int32_t, hipStream_t, hipEvent_t, hipEvent_t); \
     template <> int step_grid<n>(int64_t);                                              \
     extern template hipError_t launch_rollout_t<n>(const Params &, const RolloutArgs &, hipStream_t, hipEvent_t, hipEvent_t); \
+    extern template int rollout_kernel_t<n>(int64_t);                                   \
     template <> bool fused_rollout<n>();                                                \
     template <> bool resident_staged<n>(int64_t);                                       \
     template <> bool step_records_t<n>();                                               \
@@ -148,6 +169,7 @@ hipError_t launch_step_loop(int n, const Params &p, int32_t *actions, int32_t st
 hipError_t launch_rollout(int n, const Params &p, const RolloutArgs &r, hipStream_t s, hipEvent_t ev0 = nullptr,
                           hipEvent_t ev1 = nullptr);
 bool fused_rollout_n(int n);
+int rollout_kernel_n(int n, int64_t num_worlds);
 bool resident_staged_n(int n, int64_t num_worlds);
 // whether k_step honours Params::rec_obs (PPO's buffer.obs record from the
 // step's row passes): the agent-lane kernel of the 2-agent game only

@@ -15,7 +15,6 @@
 // The C/D layout (col = l & 15, row = 4q + i) puts a row's 32 outputs on the 16
 // lanes of one quarter-wave: LayerNorm is a 4-step xor butterfly there.
 #include <hip/hip_runtime.h>
-#include <cstdlib>
 #include "bb_launch.h"
 #include "bb_policy.h"
 #include "bb_policy_dev.h"
@@ -335,7 +334,7 @@ inline PolicyWgGrid policy_wg_grid(int64_t tiles)
 // us per launch): 16 384 rows MT 1 10.9 / MT 2 12.6 / MT 4 17.5; 24 576
 // 14.2 / 13.9 / 19.6; 32 768 16.4 / 15.3 / 19.9; 49 152 24.3 / 27.6 / 22.0;
 // 65 536 27.0 / 27.7 / 23.5 -- MT 2 while its waves (276 registers, one per
-// SIMD) fit one round, MT 4 above.  MADRONA_BB_POLICY_MT forces one (A/B).
+// SIMD) fit one round, MT 4 above.
 #ifndef POLICY_MT2_ROWS
 #define POLICY_MT2_ROWS 20480
 #endif
@@ -344,12 +343,6 @@ inline PolicyWgGrid policy_wg_grid(int64_t tiles)
 #endif
 inline int policy_mt(int64_t rows)
 {
-    static const int forced = [] {
-        const char *e = getenv("MADRONA_BB_POLICY_MT");
-        const int m = e && *e ? atoi(e) : 0;
-        return (m == 1 || m == 2 || m == 4) ? m : 0;
-    }();
-    if (forced) return forced;
     return rows < POLICY_MT2_ROWS ? 1 : (rows < POLICY_MT4_ROWS ? 2 : 4);
 }
 
@@ -361,13 +354,8 @@ static hipError_t launch_policy_mt(const PolicyArgs &a, hipStream_t s)
     // grid-stride beyond this many waves: 64-row tiles one wave per SIMD
     // (1 024 on the 256 CUs), the next tile's rows loaded under this one's
     // network (131 072 rows: 46.8 -> 43.5 us argmax, 57.1 -> 54.4 sampled;
-    // profiles/r03/ah_policy_grid_ab.txt); MADRONA_BB_POLICY_GRID overrides
-    static const int64_t forced = [] {
-        const char *e = getenv("MADRONA_BB_POLICY_GRID");
-        const long g = e && *e ? atol(e) : 0;
-        return (int64_t)(g > 0 ? g : 0);
-    }();
-    const int64_t cap = forced ? forced : (MT == 4 ? 1024 : 16384);
+    // profiles/r03/ah_policy_grid_ab.txt)
+    const int64_t cap = MT == 4 ? 1024 : 16384;
     const unsigned grid = (unsigned)(tiles < cap ? tiles : cap);
     hipLaunchKernelGGL(k_policy<MT>, dim3(grid), dim3(64), 0, s, a);
     return hipGetLastError();
@@ -376,19 +364,14 @@ static hipError_t launch_policy_mt(const PolicyArgs &a, hipStream_t s)
 // k_policy_wg from POLICY_WG_MIN_ROWS rows on: measured (profiles/r03/ap_policy_ab.txt)
 // 131 072 rows 43.2 -> 38.4 us argmax, 53.9 -> 49.1 sampled; at 65 536 rows the
 // register-weight kernel is ahead (25.3 vs 27.1, 30.3 vs 34.3: its 64-row
-// tiles amortise the bucket pass's per-tile exchanges).  MADRONA_BB_POLICY_WG=1 / 0
-// forces it on / off; MADRONA_BB_POLICY_MT forces a register-weight kernel.
+// tiles amortise the bucket pass's per-tile exchanges).  DIAG_POLICY_WG = 1 / 0
+// forces it on / off (tests).
 #ifndef POLICY_WG_MIN_ROWS
 #define POLICY_WG_MIN_ROWS 98304
 #endif
 static bool policy_wg_enabled(int64_t rows)
 {
-    static const int forced = [] {
-        const char *e = getenv("MADRONA_BB_POLICY_WG");
-        const char *m = getenv("MADRONA_BB_POLICY_MT");
-        if (m && *m) return 0;
-        return e && *e ? (atoi(e) != 0 ? 1 : 0) : -1;
-    }();
+    const int forced = diag_or(DIAG_POLICY_WG, -1);
     return forced >= 0 ? forced == 1 : rows >= POLICY_WG_MIN_ROWS;
 }
 

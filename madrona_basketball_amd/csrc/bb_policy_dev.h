@@ -206,22 +206,13 @@ __device__ __forceinline__ void bucket_noise(BucketNoise<R> &n, uint32_t seed, u
 // R rows (8, 16 or 32) over the wave's 64 lanes.  act_local (optional): row
 // r's six actions also into act_local[r] (LDS).  pre (optional): this
 // lane's uniforms, drawn ahead by bucket_noise with a's seed and step.
-// ts (diagnostics, optional): lane 0 writes the clock after the maxima, the
-// per-logit part, the per-bucket part and the outputs into ts[0..3].
-__device__ __forceinline__ void bucket_stamp(uint64_t *ts, int i, int lane)
-{
-    if (ts) {
-        const uint64_t c = wall_clock64();
-        if (lane == 0) ts[i] = c;
-    }
-}
 // PRE (compile-time, so that the uniforms stay in registers: a runtime-null
 // pointer to them would put them in scratch): `pre` holds this lane's draws.
 // STOCH: -1 a.stochastic at run time, 0 / 1 fixed at compile time.
 template <int R, bool PRE = false, int STOCH = -1>
 __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
                                                    BucketLds<R> &buf, int32_t (*act_local)[6] = nullptr,
-                                                   const BucketNoise<R> *pre = nullptr, uint64_t *ts = nullptr)
+                                                   const BucketNoise<R> *pre = nullptr)
 {
     static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
     constexpr int LPR = 64 / R;
@@ -244,7 +235,6 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     // their sum in logit order, the action (first maximum, or the inverse-CDF
     // draw over the terms in logit order), logit[a] - (max + log(sum)) --
     // pol_bucket_term's operations, the terms never leave the registers
-    bucket_stamp(ts, 0, lane);
     // round j: every lane's bucket part + LPR j; the loops run to the largest
     // bucket of the round (compile time: 8, then 3 and 2 at LPR 2), not to 8
     const auto round = [&](auto jc) {
@@ -306,8 +296,6 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     round(std::integral_constant<int, 1>());
     round(std::integral_constant<int, 2>());
     pol_wave_sync();
-    bucket_stamp(ts, 1, lane);
-    bucket_stamp(ts, 2, lane);
     if (part == 0 && live) {
         float term[POL_BUCKETS];
         int32_t act[POL_BUCKETS];
@@ -335,7 +323,6 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
             a.done_out[rr] = a.done_src[rr * a.rd_stride];
         }
     }
-    bucket_stamp(ts, 3, lane);
 }
 
 // The network's weights in LDS, shared by the waves of a workgroup (k_policy_wg,

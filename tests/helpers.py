@@ -25,15 +25,20 @@ EXACT_COLUMNS = {
 FLOAT_ATOL = 1e-5
 
 
-def sim_np(sim, name: str) -> np.ndarray:
-    return sim._views[name].detach().cpu().numpy()
+def sim_np(sim, name: str, world=None) -> np.ndarray:
+    v = sim._views[name]
+    if world is not None:
+        v = v[world:world + 1]
+    return v.detach().cpu().numpy()
 
 
-def compare(sim, oracle: Oracle, names=ALL_COLUMNS, atol: float = FLOAT_ATOL):
-    """Return ({name: description} of mismatches, {name: bit-identical fraction})."""
+def compare(sim, oracle: Oracle, names=ALL_COLUMNS, atol: float = FLOAT_ATOL, world=None):
+    """Return ({name: description} of mismatches, {name: bit-identical fraction}).
+    world: compare only that world of the simulator with a one-world oracle
+    (Oracle(1, world_offset=world), the same global world index)."""
     bad, ident = {}, {}
     for n in names:
-        a = sim_np(sim, n)
+        a = sim_np(sim, n, world)
         b = oracle.export(n)
         if a.shape != b.shape:
             bad[n] = f"shape {a.shape} vs {b.shape}"

@@ -104,3 +104,20 @@ def test_algorithmic_bytes(L):
     assert L.bb_algorithmic_bytes_per_world(2) == 1512
     assert L.bb_algorithmic_bytes_per_world(10) == 19752
     assert L.bb_obs_width(2) == 128 and L.bb_obs_width(4) == 184 and L.bb_obs_width(10) == 424
+
+
+def test_kernel_choices_are_not_read_from_the_environment(L):
+    """The library picks its kernels by its own rules; the only overrides are
+    the diagnostic bb_diag_set table (tests, A/B timing).  Its one environment
+    variable is BB_CPU_THREADS (the host executor's thread count)."""
+    from madrona_basketball_amd._lib import DIAG_KEYS, LIB_PATH
+    blob = open(LIB_PATH, "rb").read()
+    names = set(re.findall(rb"(?:MADRONA_BB|BB)_[A-Z0-9_]{3,}", blob))
+    env_like = {n for n in names if n.startswith(b"MADRONA_BB_")}
+    assert not env_like, env_like
+    assert b"BB_CPU_THREADS" in blob
+    # every key accepted, restored with -1; out-of-range keys / values refused
+    for k in DIAG_KEYS.values():
+        assert L.bb_diag_set(k, -1) == 0
+    assert L.bb_diag_set(len(DIAG_KEYS), 0) < 0 and L.bb_diag_set(0, -2) < 0
+    assert b"bb_diag_set" in L.bb_last_error()

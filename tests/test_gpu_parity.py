@@ -82,42 +82,32 @@ def test_gpu_staged_loop_kernel_equals_per_step_launches(W, n, kind):
         assert torch.equal(a._views[name], b._views[name]), name
 
 
-STAGED_CHILD = r"""
-import hashlib, torch
-from madrona_basketball_amd import ExecMode
-from tests.helpers import make_sim
-h = hashlib.sha256()
-for W, n, N in [(65536, 20, 2), (3001, 40, 2), (16384, 12, 4), (65536, 6, 4), (1000, 10, 10), (777, 12, 6),
-                (5000, 9, 8)]:
-    sim = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
-    staged = sim.stage_random_actions(n, action_seed=12, step0=0)
-    sim.step_n_staged(staged)
-    torch.cuda.synchronize()
-    h.update(staged.cpu().numpy().tobytes())
-    for name in sorted(sim._views):
-        h.update(sim._views[name].cpu().numpy().tobytes())
-print("HASH", h.hexdigest())
-"""
+def _staged_hash(kind: int) -> str:
+    import hashlib
+    from madrona_basketball_amd import _lib
+    h = hashlib.sha256()
+    with _lib.diag(step_loop=kind):
+        for W, n, N in [(65536, 20, 2), (3001, 40, 2), (16384, 12, 4), (65536, 6, 4), (1000, 10, 10), (777, 12, 6),
+                        (5000, 9, 8)]:
+            sim = make_sim(ExecMode.CUDA, W, num_agents=N, per_world_rng=True)
+            staged = sim.stage_random_actions(n, action_seed=12, step0=0)
+            sim.step_n_staged(staged)
+            torch.cuda.synchronize()
+            h.update(staged.cpu().numpy().tobytes())
+            for name in sorted(sim._views):
+                h.update(sim._views[name].cpu().numpy().tobytes())
+            del sim, staged
+    return h.hexdigest()
 
 
 def test_gpu_staged_loop_kernel_write_backs():
     """The staged action rows after the call (the defence AI's overrides written
-    back) and every column: the register-resident loop (MADRONA_BB_STEP_LOOP=2)
-    and k_step_loop (1) == one k_step launch per step (0; read once per
-    process: child processes), at 2 agents and -- the loop forced on up to 10
-    agents -- the shared-world step."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    out = {}
-    for loop in ("2", "1", "0"):
-        env = dict(os.environ, MADRONA_BB_STEP_LOOP=loop, MADRONA_BB_STEP_LOOP_MAX_N="10", PYTHONPATH=root)
-        r = subprocess.run([sys.executable, "-c", STAGED_CHILD], cwd=root, env=env, capture_output=True, text=True,
-                           timeout=240)
-        assert r.returncode == 0, r.stderr[-3000:]
-        out[loop] = [l for l in r.stdout.splitlines() if l.startswith("HASH")][-1]
-    assert out["2"] == out["0"] and out["1"] == out["0"], out
+    back) and every column: the register-resident loop (kind 2, at N >= 4 the
+    shared-world resident kernel while the step fits the Infinity Cache, else
+    k_step_loop) and k_step_loop (1) == one k_step launch per step (0), at 2, 4,
+    6, 8 and 10 agents."""
+    out = {kind: _staged_hash(kind) for kind in (2, 1, 0)}
+    assert out[2] == out[0] and out[1] == out[0], out
 
 
 def test_gpu_tag_heavy_rollout():

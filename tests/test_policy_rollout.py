@@ -125,28 +125,16 @@ def test_gpu_fused_policy_rollout_equals_per_step_launches(native_lib, W, n, tra
         assert torch.equal(sims[0]._views[name], sims[1]._views[name]), name
 
 
-PWAVES_CHILD = r"""
-from tests.test_policy_rollout import test_gpu_fused_policy_rollout_equals_per_step_launches as t
-for W, n, tr, st in [(8192, 12, 1, True), (1000, 10, 0, False), (16384, 6, 0, True)]:
-    t(None, W, n, tr, st)
-print("PWAVES_OK")
-"""
-
-
 @pytest.mark.gpu
-@pytest.mark.parametrize("pw", ["2", "4"])
+@pytest.mark.parametrize("pw", [2, 4])
 def test_gpu_fused_policy_rollout_policy_wave_counts(native_lib, pw):
     """k_rollout_policy with its policy waves forced to 2 (one per M-tile) or 4
-    (two per M-tile, one output half each) at any grid (MADRONA_BB_PPO_PWAVES,
-    read once per process: a child process) == the per-step launches."""
-    import os
-    import subprocess
-    import sys
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MADRONA_BB_PPO_PWAVES=pw, PYTHONPATH=root)
-    r = subprocess.run([sys.executable, "-c", PWAVES_CHILD], cwd=root, env=env, capture_output=True, text=True,
-                       timeout=300)
-    assert r.returncode == 0 and "PWAVES_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    (two per M-tile, one output half each) at any grid (the ppo_pwaves path
+    override) == the per-step launches."""
+    from madrona_basketball_amd import _lib
+    with _lib.diag(ppo_pwaves=pw):
+        for W, n, tr, st in [(8192, 12, 1, True), (1000, 10, 0, False), (16384, 6, 0, True)]:
+            test_gpu_fused_policy_rollout_equals_per_step_launches(native_lib, W, n, tr, st)
 
 
 @pytest.mark.gpu

@@ -2,34 +2,28 @@
 policy pass fused behind the world step (bb_rollout_policy above 16 384 worlds;
 scripts/ppo.py:65-134 over scripts/env.py:126-170), the whole rollout in one
 launch (each wave steps its worlds K times; default) or one launch per step
-(MADRONA_BB_PPO_STEP_LOOP=0, child process).  Every recorded output
+(the ppo_step_loop path override = 0).  Every recorded output
 (buffer.obs / actions / log_probs / values / rewards / not_dones, next_value)
 and every simulator column must equal the per-step launches (k_policy +
 k_step, the `per_step` flag) and the loop of FusedPolicy.act + step, bit for
 bit: the row passes feed layer 1's MFMA chain in its own k order, so the
 policy sees the same floats in the same order.
 
-The fused step is taken by row count (MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS,
-read once per process): small and ragged grids run it in a child process with
-the bound lowered to 1 (partial waves, inactive waves of the last workgroup,
-4-wave workgroups)."""
-import os
-import subprocess
-import sys
-
+The fused step is taken by row count: small and ragged grids run it with the
+path overrides ppo_step_fused_min_worlds = 1 and ppo_fused_max_worlds = 0
+(partial waves, inactive waves of the last workgroup, 4-wave workgroups)."""
 import pytest
 import torch
 
-from madrona_basketball_amd import ExecMode
+from madrona_basketball_amd import ExecMode, _lib
 from madrona_basketball_amd.policy import FusedPolicy, make_agent
 from tests.helpers import make_sim
 from tests.test_policy_rollout import assert_same, reference_loop, run_pair
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def fused_vs_per_step(W, n, trainee, stochastic, seed=7, step0=3, partial=False):
-    sims = [make_sim(ExecMode.CUDA, W, per_world_rng=True) for _ in range(2)]
+def fused_vs_per_step(W, n, trainee, stochastic, seed=7, step0=3, partial=False, flags=None):
+    sims = [make_sim(ExecMode.CUDA, W, per_world_rng=True, **(flags or {})) for _ in range(2)]
     for s in sims:
         s.step_n(9, random_actions=True, action_seed=321, step0=0)
     pol = FusedPolicy.from_agent(make_agent(5).cuda())
@@ -78,42 +72,38 @@ def test_gpu_fused_ppo_step_single_step(native_lib):
     fused_vs_per_step(65536, 1, 1, True)
 
 
-CHILD = r'''
-import torch
-from tests.test_ppo_step import fused_vs_per_step
-for W, n, trainee, stoch in [(1000, 6, 1, True), (64, 3, 0, False), (12345, 5, 0, True), (31, 4, 1, True),
-                             (8192, 4, 0, True)]:
-    fused_vs_per_step(W, n, trainee, stoch)
-print("PPO_STEP_OK")
-'''
-
-
 @pytest.mark.gpu
 def test_gpu_fused_ppo_step_forced_on_small_grids(native_lib):
-    env = dict(os.environ, MADRONA_BB_PPO_STEP_FUSED_MIN_WORLDS="1", MADRONA_BB_PPO_FUSED_MAX_WORLDS="0",
-               PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-c", CHILD], cwd=ROOT, env=env, capture_output=True, text=True,
-                       timeout=240)
-    assert r.returncode == 0 and "PPO_STEP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
-
-
-STEP_LAUNCHES_CHILD = r'''
-import torch
-from tests.test_ppo_step import fused_vs_per_step
-for W, n, trainee, stoch in [(65536, 6, 1, True), (40001, 4, 0, True), (65536, 1, 0, False)]:
-    fused_vs_per_step(W, n, trainee, stoch)
-print("PPO_STEP_OK")
-'''
+    with _lib.diag(ppo_step_fused_min_worlds=1, ppo_fused_max_worlds=0):
+        for W, n, trainee, stoch in [(1000, 6, 1, True), (64, 3, 0, False), (12345, 5, 0, True), (31, 4, 1, True),
+                                     (8192, 4, 0, True)]:
+            fused_vs_per_step(W, n, trainee, stoch)
 
 
 @pytest.mark.gpu
 def test_gpu_fused_ppo_step_one_launch_per_step(native_lib):
-    """MADRONA_BB_PPO_STEP_LOOP=0: one k_step_ppo launch per step, equal to the
+    """ppo_step_loop = 0: one k_step_ppo launch per step, equal to the
     per-step launches (and so to the one-launch rollout)."""
-    env = dict(os.environ, MADRONA_BB_PPO_STEP_LOOP="0", PYTHONPATH=ROOT)
-    r = subprocess.run([sys.executable, "-c", STEP_LAUNCHES_CHILD], cwd=ROOT, env=env, capture_output=True,
-                       text=True, timeout=240)
-    assert r.returncode == 0 and "PPO_STEP_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    with _lib.diag(ppo_step_loop=0):
+        for W, n, trainee, stoch in [(65536, 6, 1, True), (40001, 4, 0, True), (65536, 1, 0, False)]:
+            fused_vs_per_step(W, n, trainee, stoch)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W,n,flags", [(8192, 700, {}), (65536, 640, {}),
+                                       (4096, 300, dict(one_on_one=False, tag_mask=False)),
+                                       (2000, 200, dict(tag_mask=False))])
+def test_gpu_fused_ppo_step_long_rollouts_and_full_game(native_lib, W, n, flags):
+    """k_rollout_ppo as one launch over 640-700 steps (every world crosses the
+    620-step clock expiry and its resetWorld inside the launch), and on the
+    full-game / grab-and-pass rules (one_on_one=False, tag_mask=False), ==
+    k_policy + k_step per step, every record and every column."""
+    with _lib.diag(ppo_step_fused_min_worlds=1, ppo_fused_max_worlds=0):
+        sims_probe = make_sim(ExecMode.CUDA, W, per_world_rng=True, **flags)
+        assert _lib.load().bb_rollout_policy_path(sims_probe._h, 0, 0) == 2  # BB_PPO_PATH_FUSED_STEP
+        del sims_probe
+        b = fused_vs_per_step(W, n, 0, True, flags=flags)
+    assert (b["done"] == 1).any()  # resets happened inside the launch
 
 
 @pytest.mark.gpu

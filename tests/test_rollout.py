@@ -274,38 +274,25 @@ def test_gpu_fused_rollout_full_size_identical_worlds(native_lib):
         assert torch.equal(flat, flat[:1].expand_as(flat)), name
 
 
-# The N >= 4 K-step rollout kernel (k_rollout_shared) is the default up to
-# MADRONA_BB_ROLLOUT_SHARED_MAX_N agents (4; read once per process): the cases
-# run in a child process with the bound at 10, so every N takes the kernel.
-MORE_AGENTS_CHILD = r"""
-import torch
-from tests.test_rollout import more_agents_fused_equals_host, more_agents_fused_equals_per_step
-for N, W, K in [(4, 700, 60), (6, 1001, 40), (8, 333, 30), (10, 777, 30)]:
-    more_agents_fused_equals_host(N, W, K)
-for N, W, K, flags in [(4, 65536, 8, dict()), (10, 8192, 12, dict()),
-                       (4, 4096, 40, dict(one_on_one=False, tag_mask=False)), (6, 2048, 24, dict(tag_mask=False))]:
-    more_agents_fused_equals_per_step(N, W, K, flags)
-print("MORE_AGENTS_OK")
-"""
-
-
 @pytest.mark.gpu
 def test_gpu_rollout_more_agents_fused(native_lib):
     """N >= 4: one k_rollout_shared launch for all K steps (the world in LDS,
-    rows from the source table) == the host executor (ragged last waves) and ==
-    K k_step launches (the per_step flag) at BASELINE configs[1]'s 65 536 worlds
-    x 4 agents and 8 192 x 10, every recorded output, every written-back action
-    and every column afterwards; the unrecorded form (rows, rewards and done
-    flags into the sim's own tensors every step) as well."""
-    import os
-    import subprocess
-    import sys
+    rows from the source table; the kernel forced on up to 10 agents by the
+    rollout_shared_max_n path override, default 4) == the host executor
+    (ragged last waves) and == K k_step launches (the per_step flag) at
+    BASELINE configs[1]'s 65 536 worlds x 4 agents and 8 192 x 10, every
+    recorded output, every written-back action and every column afterwards;
+    the unrecorded form (rows, rewards and done flags into the sim's own
+    tensors every step) as well."""
+    from madrona_basketball_amd import _lib
     _gpu()
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, MADRONA_BB_ROLLOUT_SHARED_MAX_N="10", PYTHONPATH=root)
-    r = subprocess.run([sys.executable, "-c", MORE_AGENTS_CHILD], cwd=root, env=env, capture_output=True, text=True,
-                       timeout=600)
-    assert r.returncode == 0 and "MORE_AGENTS_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    with _lib.diag(rollout_shared_max_n=10):
+        for N, W, K in [(4, 700, 60), (6, 1001, 40), (8, 333, 30), (10, 777, 30)]:
+            more_agents_fused_equals_host(N, W, K)
+        for N, W, K, flags in [(4, 65536, 8, dict()), (10, 8192, 12, dict()),
+                               (4, 4096, 40, dict(one_on_one=False, tag_mask=False)),
+                               (6, 2048, 24, dict(tag_mask=False))]:
+            more_agents_fused_equals_per_step(N, W, K, flags)
 
 
 @pytest.mark.gpu
