@@ -282,7 +282,9 @@ int bb_rollout_policy(bb_sim *sim, const bb_policy_weights *w, const bb_policy_w
 
 /* The implementation bb_rollout_policy takes on this simulator, and the
  * algorithmic bytes of one call of n steps with every output recorded (the
- * bytes that path must move: HBM roofline of the PPO loop). */
+ * bytes that path must move: HBM roofline of the PPO loop).
+ * On a simulator of other than 2 agents both fail: BB_ERR_UNSUPPORTED (< 0),
+ * bb_last_error() says why. */
 #define BB_PPO_PATH_HOST 0          /* CPU mode: the host executor */
 #define BB_PPO_PATH_FUSED_ROLLOUT 1 /* one k_rollout_policy launch for all n steps */
 #define BB_PPO_PATH_FUSED_STEP 2    /* a policy launch, then k_rollout_ppo (step + next policy pass, n times) */

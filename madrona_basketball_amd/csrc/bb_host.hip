@@ -602,6 +602,32 @@ int bb_write_random_actions(bb_sim *s, uint32_t action_seed, uint32_t step, void
     return bb::host_random_actions(s->n, s->p, *s->pool, action_seed, step);
 }
 
+}  // extern "C"
+
+// The hipEvent_t of a timed call (kernel_ms), destroyed on every exit.
+struct EventVec {
+    std::vector<hipEvent_t> ev;
+    ~EventVec()
+    {
+        for (hipEvent_t e : ev)
+            if (e) (void)hipEventDestroy(e);
+    }
+    hipError_t create(size_t n)
+    {
+        ev.assign(n, nullptr);
+        for (auto &e : ev) {
+            const hipError_t r = hipEventCreate(&e);
+            if (r != hipSuccess) {
+                e = nullptr;
+                return r;
+            }
+        }
+        return hipSuccess;
+    }
+};
+
+extern "C" {
+
 int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed, uint32_t step0,
               void *stream, float *kernel_ms)
 {
@@ -615,13 +641,11 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
     }
     DeviceGuard g(s->device);
     hipStream_t st = (hipStream_t)stream;
-    std::vector<hipEvent_t> ev;
+    EventVec evs;
+    std::vector<hipEvent_t> &ev = evs.ev;
     if (kernel_ms && n > 0) {
-        ev.resize((size_t)2 * n);
-        for (auto &e : ev) {
-            hipError_t he = hipEventCreate(&e);
-            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
-        }
+        const hipError_t he = evs.create((size_t)2 * n);
+        if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
     }
     for (int32_t k = 0; k < n; k++) {
         if (random_actions) {
@@ -642,7 +666,6 @@ int bb_step_n(bb_sim *s, int32_t n, int32_t random_actions, uint32_t action_seed
             (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
             total += ms;
         }
-        for (auto &x : ev) (void)hipEventDestroy(x);
         *kernel_ms = (float)total;
     }
     return BB_OK;
@@ -739,13 +762,11 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
     const int kind = staged_path(s, n);
     const bool loop = kind != BB_STAGED_PER_STEP;
     const bool resident = kind == BB_STAGED_RESIDENT;
-    std::vector<hipEvent_t> ev;
+    EventVec evs;
+    std::vector<hipEvent_t> &ev = evs.ev;
     if (kernel_ms && n > 0) {
-        ev.resize((size_t)2 * (loop ? 1 : n));
-        for (auto &e : ev) {
-            hipError_t he = hipEventCreate(&e);
-            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
-        }
+        const hipError_t he = evs.create((size_t)2 * (loop ? 1 : n));
+        if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
     }
     if (resident) {
         bb::RolloutArgs r{actions, s->p.c.obs, s->p.c.reward, s->p.c.done, 0, 0, n, 1};
@@ -776,7 +797,6 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
             (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
             total += ms;
         }
-        for (auto &x : ev) (void)hipEventDestroy(x);
         *kernel_ms = (float)total;
     }
     return BB_OK;
@@ -832,13 +852,11 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
     hipStream_t st = (hipStream_t)stream;
     const bool fused = !(flags & BB_ROLLOUT_PER_STEP) && bb::fused_rollout_n(s->n);
     const int32_t launches = fused ? 1 : n;
-    std::vector<hipEvent_t> ev;
+    EventVec evs;
+    std::vector<hipEvent_t> &ev = evs.ev;
     if (kernel_ms) {
-        ev.resize((size_t)2 * launches);
-        for (auto &e : ev) {
-            hipError_t he = hipEventCreate(&e);
-            if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
-        }
+        const hipError_t he = evs.create((size_t)2 * launches);
+        if (he != hipSuccess) return hip_fail(he, "hipEventCreate");
     }
     hipEvent_t *evp = ev.empty() ? nullptr : ev.data();
     if (fused) {
@@ -876,7 +894,6 @@ int bb_rollout(bb_sim *s, int32_t n, int32_t *actions, float *obs_out, float *re
             (void)hipEventElapsedTime(&ms, ev[2 * k], ev[2 * k + 1]);
             total += ms;
         }
-        for (auto &x : ev) (void)hipEventDestroy(x);
         *kernel_ms = (float)total;
     }
     return BB_OK;
@@ -1593,12 +1610,15 @@ int64_t bb_rollout_state_bytes_per_world(int32_t n)
 int32_t bb_rollout_policy_path(const bb_sim *s, int32_t with_opponent, uint32_t flags)
 {
     if (!s) return fail(BB_ERR_INVALID_ARG, "bb_rollout_policy_path: sim");
-    return ppo_path(s, with_opponent != 0, flags);
+    const int32_t path = ppo_path(s, with_opponent != 0, flags);
+    if (path < 0) return fail(BB_ERR_UNSUPPORTED, "bb_rollout_policy_path: the reference's 2-agent game only");
+    return path;
 }
 
 int64_t bb_rollout_policy_bytes(const bb_sim *s, int32_t with_opponent, uint32_t flags, int32_t n)
 {
-    if (!s || n < 1 || s->n != 2) return 0;
+    if (!s || n < 1) return 0;
+    if (s->n != 2) return fail(BB_ERR_UNSUPPORTED, "bb_rollout_policy_bytes: the reference's 2-agent game only");
     const int64_t B = bb_algorithmic_bytes_per_world(2);
     const int64_t row = 4 * (int64_t)bb::obs_used(2);   // a sim observation row's values (412 B)
     const int64_t rec = 4 * (int64_t)bb::POL_IN;        // a buffer.obs row (128 floats)
@@ -1613,12 +1633,13 @@ int64_t bb_rollout_policy_bytes(const bb_sim *s, int32_t with_opponent, uint32_t
         // step the policy's records and the step's reward / done
         return B + (int64_t)n * (rec + outs + rd) + 4;
     case BB_PPO_PATH_FUSED_STEP:
-        // steps 0..n-2: the world step without sim rows (neither agent's is
-        // read before the last step rewrites them), the trainee's row into
-        // buffer.obs[k+1], the action row into the sim, the outputs, the
-        // reward / done; the last step: the whole world step, reward / done,
-        // next_value
-        return pass0 + (int64_t)(n - 1) * (B - 2 * row + rec + 24 + outs + rd) + B + rd + 4;
+        // what the call must move, not what the launch does: the state in once
+        // and out once (B, the last step's rows included), the trainee's rows
+        // read by the first policy pass, per step the records, the value pass's
+        // next_value.  (k_rollout_ppo also round-trips each step's state and
+        // action rows through memory -- L2 hits mostly, its PMC traffic is
+        // 2x these bytes -- which the fused rollout's registers avoid.)
+        return B + rec + (int64_t)n * (rec + outs + rd) + 4;
     default:
         // per step: the world step (the trainee's row into buffer.obs[k+1]
         // instead of the sim from step 0 to n-2), then a policy pass reading
