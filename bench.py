@@ -677,6 +677,8 @@ def main():
         if loop_main and one_launch_s is not None:
             pc["kernel_avg_us"] = one_launch_s * 1e6
             pc["frac"] = out["roofline"]["one_launch_per_step"]["frac"]
+            pc["algorithmic_bytes_per_launch"] = L.bb_algorithmic_bytes_per_world(args.agents) * W
+            pc["traffic"] = load_traffic(f"W{W}_N{args.agents}_per_call")
         out["per_call_step"] = pc
         out["headline"] = ("value = the staged steps as one launch (" + out["roofline"]["kernel"] + "); every step "
                            "stores all its outputs as a per-call step does, but no consumer runs between steps: an "
