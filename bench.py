@@ -48,6 +48,16 @@ def _cpu_worker(job):
     return worlds, steps, elapsed
 
 
+def cpu_model() -> str:
+    """The host CPU's model name and thread count (SURVEY §8(d) asks for both)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            names = [l.split(":", 1)[1].strip() for l in f if l.startswith("model name")]
+        return f"{names[0]} ({len(names)} threads visible)" if names else "unknown"
+    except OSError:
+        return "unknown"
+
+
 def cpu_baseline(num_agents: int, seconds: float, procs: int):
     """The oracle on `procs` host cores (one process each, spawned before this
     process touches the GPU), each on a bounded sample of the same workload;
@@ -61,7 +71,7 @@ def cpu_baseline(num_agents: int, seconds: float, procs: int):
             res = pool.map(_cpu_worker, [(num_agents, seconds, worlds)] * procs)
     value = sum(w * st / el for w, st, el in res)
     steps = min(st for _, st, _ in res)
-    return {"value": value, "unit": "env-steps/s", "cores": procs, "kind": "port",
+    return {"value": value, "unit": "env-steps/s", "cores": procs, "kind": "port", "cpu_model": cpu_model(),
             "sample": f"{procs} process(es) x {worlds} worlds x >= {steps} steps each, {num_agents} agents, "
                       f"threefry random actions, ~{seconds:.0f} s per process, rates summed"}
 

@@ -156,3 +156,19 @@ def test_gpu_env_py_call_sequence_matches_oracle(agent_idx):
                 check(out)
             bad, _ = compare(sim, o)
             assert not bad, (it, bad)
+
+
+@pytest.mark.parametrize("W", [4194304, 4194303])
+def test_gpu_maximum_size_staged_and_per_call(W):
+    """Maximum sizes: 4 194 304 worlds (7 GB of state and rows, 8.4 M agent
+    rows) and a ragged 4 194 303 -- the resident loop (one launch, 24 steps) ==
+    24 k_step launches in every column and write-back, and sampled worlds
+    (the last one included) == the oracle."""
+    a, rows_a = staged_run(W, [(24, 0)], 2)
+    b, rows_b = staged_run(W, [(24, 0)], 0)
+    for name in a._views:
+        assert torch.equal(a._views[name], b._views[name]), name
+    assert torch.equal(rows_a[0], rows_b[0])
+    del rows_a, rows_b, b
+    torch.cuda.empty_cache()
+    sampled_worlds_match_oracle(a, W, 24, count=8)
