@@ -2770,13 +2770,17 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
     if constexpr (N != 2 || !FusedRollout<N>::value) {
         return hipErrorNotSupported;
     } else {
-        // 4 policy waves while the grid is at most one workgroup per CU (8 192
-        // worlds: 9.66 -> 9.48 us per step, profiles/r05/ad_pw_ab.txt), 2 above
-        // (16 384: 12.1 vs 18.2); DIAG_PPO_PWAVES = 2 / 4 forces it (tests).
-        // (3 waves: each its own SIMD; 5 waves share them -- the 256-register budget)
+        // 2 policy waves (3 waves per workgroup: each its own SIMD, the sim
+        // wave with the SIMD's whole register file, no scratch).  4 (5 waves:
+        // two share a SIMD, the 256-register budget, 45 spilled VGPRs and a
+        // scratch launch) measured ahead at 8 192 worlds in round 5 (9.66 ->
+        // 9.48 us per step, profiles/r05/ad_pw_ab.txt) and behind in round 6
+        // (9.80 vs 9.62, three interleaved pairs, profiles/r06/o_ppo_pw_ab.txt;
+        // per call 22.3 + 8.99 us per step vs 18.9 + 8.84); 16 384: 18.2 vs 12.1.
+        // DIAG_PPO_PWAVES = 2 / 4 forces it (tests).
         const dim3 grid((unsigned)((p.num_worlds + 31) / 32));
         const int forced = diag_or(DIAG_PPO_PWAVES, 0);
-        const int pw = forced == 2 || forced == 4 ? forced : (grid.x <= device_cus() ? 4 : 2);
+        const int pw = forced == 2 || forced == 4 ? forced : 2;
         if (pw == 4)
             hipLaunchKernelGGL(HIP_KERNEL_NAME(k_rollout_policy<N, 2, 4>), grid, dim3(WAVE * 5), 0, s, p, r);
         else if (grid.x <= device_cus())
