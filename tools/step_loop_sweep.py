@@ -26,9 +26,12 @@ def main():
     ap.add_argument("--agents", type=int, default=2)
     ap.add_argument("--kinds", default="2,1,0")
     ap.add_argument("--check", action="store_true")
+    ap.add_argument("--minw", type=int, default=-1, help="rollout_minw path override (3: k_rollout2)")
     a = ap.parse_args()
     kinds = [int(x) for x in a.kinds.split(",")]
     L = _lib.load()
+    if a.minw >= 0:
+        _lib.diag_set("rollout_minw", a.minw)
     for W in [int(x) for x in a.worlds.split(",")]:
         sim = mba.SimpleGridworldSimulator(32, 17, 15.7575, 8.382, 39600, mba.ExecMode.CUDA, W, 0,
                                            num_agents=a.agents, per_world_rng=True)
@@ -63,7 +66,7 @@ def main():
                 del acts
             res[kind] = statistics.median(ts)
         L.bb_diag_step_loop(-1)
-        print(f"worlds {W:7d} x {a.agents}  " + "   ".join(f"kind {k} {res[k]:8.2f} us/step" for k in kinds),
+        print(f"worlds {W:7d} x {a.agents} minw {a.minw} {_lib.kernel_name(sim._h, 1, a.steps)}  " + "   ".join(f"kind {k} {res[k]:8.2f} us/step" for k in kinds),
               flush=True)
         del sim
         torch.cuda.empty_cache()
