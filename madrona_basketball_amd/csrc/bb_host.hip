@@ -783,7 +783,7 @@ int bb_step_n_staged(bb_sim *s, int32_t n, int32_t *actions, void *stream, float
                                   : bb::launch_step(s->n, pp, st, bb::MODE_FULL, ev[2 * k], ev[2 * k + 1]);
         if (e != hipSuccess) return hip_fail(e, "launch step kernel");
     }
-    if (n > 0) {
+    if (n > 0 && !resident) {  // (the resident loop stores the last step's rows there itself)
         hipError_t e = hipMemcpyAsync(s->p.c.action, actions + (int64_t)(n - 1) * rows, (size_t)rows * 4,
                                       hipMemcpyDeviceToDevice, st);
         if (e != hipSuccess) return hip_fail(e, "copy last actions");

@@ -793,6 +793,18 @@ __device__ __forceinline__ void rollout_agent_lanes(const Params &p, const Rollo
         store_world_agent(v, p, w_s * N + k, 0);
         if (k == 0) store_world_shared(v, p, w_s);  // world fields are not permuted in a view
     }
+    if (STORE && active && r.steps > 0) {
+        // the last step's action rows (overrides included) into the sim's
+        // action tensor, as bb_step_n_staged leaves it (no copy launch after
+        // the kernel): read back from the staged rows this lane stored last
+        // (after the loop: nothing of the step waits on this load)
+        int64_t w_s = w;
+        __asm__ volatile("" : "+v"(w_s));
+        const int64_t row = w_s * N + lane % N;
+        uint32_t a[6];
+        load_words<6>(r.actions + (int64_t)(r.steps - 1) * rows * 6, row, a);
+        store_words<6>(p.c.action, row, a);
+    }
 }
 
 // MINW: waves per SIMD the register budget is sized for.  2 (256 registers)
@@ -917,6 +929,14 @@ __device__ __forceinline__ void split_sim_wave(const Params &p, const RolloutArg
         const int k = lane % N;
         store_world_agent(v, p, w_s * N + k, 0);
         if (k == 0) store_world_shared(v, p, w_s);
+    }
+    if (STORE && active && r.steps > 0) {  // the last step's action rows into the sim's action tensor
+        int64_t w_s = w;
+        __asm__ volatile("" : "+v"(w_s));
+        const int64_t row = w_s * N + lane % N;
+        uint32_t a[6];
+        load_words<6>(r.actions + (int64_t)(r.steps - 1) * rows * 6, row, a);
+        store_words<6>(p.c.action, row, a);
     }
 }
 
@@ -2386,6 +2406,15 @@ __device__ __forceinline__ void rollout_shared_world(const Params &p, const Roll
             }
             __syncthreads();
         }
+    }
+    if (STORE && active && r.steps > 0) {  // the last step's action rows into the sim's action tensor
+        int k_e = k;
+        int64_t w_e = w;
+        __asm__ volatile("" : "+v"(k_e));
+        __asm__ volatile("" : "+v"(w_e));
+        uint32_t a6[6];
+        load_words<6>(r.actions + (int64_t)(r.steps - 1) * p.num_worlds * N * 6, w_e * N + k_e, a6);
+        store_words<6>(p.c.action, w_e * N + k_e, a6);
     }
     // the state after the last step, every column (the per-step launches'
     // last stores; actions / rewards / done flags as the last step left them)
