@@ -17,8 +17,12 @@ def load_math_probe():
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < max(os.path.getmtime(SRC), os.path.getmtime(HDR)):
         # -mfma (where the CPU has it) only speeds up fma_d; fma is exact either way
         fma = ["-mfma"] if "fma" in open("/proc/cpuinfo").read().split() else []
+        # built under a per-process name and renamed into place: concurrent
+        # test workers never load a half-written library
+        tmp = f"{LIB}.{os.getpid()}.tmp"
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
-                        *fma, "-pthread", "-o", LIB, SRC, "-lm"], check=True)
+                        *fma, "-pthread", "-o", tmp, SRC, "-lm"], check=True)
+        os.replace(tmp, LIB)
     L = ctypes.CDLL(LIB)
     L.exhaustive_mismatches.restype = ctypes.c_int64
     L.exhaustive_double_mismatches.restype = ctypes.c_int64
