@@ -4,6 +4,7 @@
 # step has its own time limit; the first failing step ends the script.
 # Usage: bash tools/gpu_r05.sh <tag> <step>...
 #   bench                      default bench line (all configs, CPU baselines)
+#   benchshort                 the driver's invocation (--gpus 1 --steps 20 --warmup 5)
 #   prof:<W>:<N>               kernel stats of k_step<N> at W worlds, that workload alone
 #   profhead                   kernel stats of the headline line's own command (default steps)
 #   profppo:<W>                kernel stats of the PPO rollout (K=32) at W worlds
@@ -45,6 +46,7 @@ for s in "$@"; do
     n=${c:-2}; sfx=${c:+_N$c}
     case $kind in
     bench) step bench 600 python3 "$R/bench.py" --steps 1000 --warmup 100 ;;
+    benchshort) step bench_short 600 python3 "$R/bench.py" --gpus 1 --steps 20 --warmup 5 ;;
     tests) step pytest_gpu 900 python3 -u -m pytest "$R/tests" -m gpu -q -rfE --timeout 300 --timeout-method thread ;;
     pytest) if [ -n "$b" ]; then
                 step "pytest_$(basename "$a" .py)" 600 python3 -u -m pytest "$R/$a" -m gpu -q -rfE -k "$b" --timeout 240 --timeout-method thread
