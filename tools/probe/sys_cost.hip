@@ -22,14 +22,14 @@ namespace bb {
     }
 BB_SYS_KERNEL(none, (void)c)
 BB_SYS_KERNEL(move, sys_move_agents(s, c, EachAgent()))
-BB_SYS_KERNEL(grab, for (int i = 0; i < N; i++) sys_grab(s, i))
+BB_SYS_KERNEL(grab, for (int i = 0; i < N; i++) sys_grab(s, c, i))
 BB_SYS_KERNEL(pass, for (int i = 0; i < N; i++) sys_pass(s, i))
 BB_SYS_KERNEL(shoot, sys_shoot(s, c, EachAgent()))
 BB_SYS_KERNEL(move_ball, sys_move_ball(s, c))
 BB_SYS_KERNEL(shot_pct, sys_shot_percentage(s, c, EachAgent()))
 BB_SYS_KERNEL(score, sys_score(s, c, 0); sys_score(s, c, 1))
 BB_SYS_KERNEL(oob, sys_out_of_bounds(s, c))
-BB_SYS_KERNEL(last_touch, sys_last_touch(s))
+BB_SYS_KERNEL(last_touch, sys_last_touch(s, c))
 BB_SYS_KERNEL(clock, sys_clock(s))
 BB_SYS_KERNEL(inbound_violation, sys_inbound_violation(s, c))
 BB_SYS_KERNEL(reset, if (s.reset_now != 0) { reset_world(s, c); s.reset_now = 0; })
