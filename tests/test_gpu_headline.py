@@ -29,14 +29,14 @@ def _need_gpu(native_lib, oracle_lib):
     assert torch.cuda.is_available(), "GPU tests selected but no HIP device is visible"
 
 
-def staged_run(W, chunks, kind):
+def staged_run(W, chunks, kind, agents=2):
     """A simulator stepped through bb_step_n_staged in `chunks` = [(steps,
-    step0)] (one call each), with the staged launch kind forced; returns the
-    simulator and every chunk's staged rows after the call (with the defence
-    AI's overrides written back)."""
-    sim = make_sim(ExecMode.CUDA, W, per_world_rng=True)
+    step0)] (one call each), with the staged launch kind forced (None: the
+    product's rule); returns the simulator and every chunk's staged rows after
+    the call (with the defence AI's overrides written back)."""
+    sim = make_sim(ExecMode.CUDA, W, num_agents=agents, per_world_rng=True)
     rows = []
-    with _lib.diag(step_loop=kind):
+    with _lib.diag(**({} if kind is None else {"step_loop": kind})):
         for n, step0 in chunks:
             acts = sim.stage_random_actions(n, action_seed=SEED, step0=step0)
             if kind == 2:
@@ -47,11 +47,11 @@ def staged_run(W, chunks, kind):
     return sim, rows
 
 
-def sampled_worlds_match_oracle(sim, W, steps, count=16):
+def sampled_worlds_match_oracle(sim, W, steps, count=16, agents=2):
     rng = np.random.default_rng(W)
     worlds = [0, W - 1] + [int(w) for w in rng.choice(np.arange(1, W - 1), size=count - 2, replace=False)]
     for w in worlds:
-        o = Oracle(1, flags=oracle_flags(per_world_rng=True), world_offset=w)
+        o = Oracle(1, num_agents=agents, flags=oracle_flags(per_world_rng=True), world_offset=w)
         for t in range(steps):
             o.random_actions(SEED, t)
             o.step()
@@ -97,6 +97,28 @@ def test_gpu_resident_loop_beyond_the_cache_700_steps():
     assert int(a.internal_tensor("cur_step").max()) < 700
     del rows_a, rows_b, b
     sampled_worlds_match_oracle(a, W, 700)
+
+
+@pytest.mark.parametrize("agents,kernel", [(4, "bb::k_rollout_shared<4, true>"), (10, "bb::k_step_loop<10>")])
+def test_gpu_more_agents_bench_configs_at_bench_length(agents, kernel):
+    """The bench line's 65 536 x 4 ("2v2", the resident shared-world loop) and
+    65 536 x 10 ("5v5", C5: the reloading step loop) objects at their timed
+    length: 20 + 200 staged steps in two launches, as bench.py's config lines
+    run them == 220 k_step launches on every column and staged write-back; 8
+    worlds == the oracle."""
+    W, chunks = 65536, [(20, 0), (200, 20)]
+    probe = make_sim(ExecMode.CUDA, W, num_agents=agents, per_world_rng=True)
+    assert _lib.kernel_name(probe._h, 1, 200) == kernel
+    del probe
+    a, rows_a = staged_run(W, chunks, None, agents)
+    b, rows_b = staged_run(W, chunks, 0, agents)
+    for name in a._views:
+        assert torch.equal(a._views[name], b._views[name]), name
+    for ra, rb in zip(rows_a, rows_b):
+        assert torch.equal(ra, rb), "staged write-backs"
+    del rows_a, rows_b, b
+    torch.cuda.empty_cache()
+    sampled_worlds_match_oracle(a, W, 220, count=8, agents=agents)
 
 
 @pytest.mark.parametrize("agent_idx", [0, 1])
