@@ -2800,9 +2800,9 @@ hipError_t launch_rollout_policy_t(const Params &p, const PolicyRolloutArgs &r, 
         return hipErrorNotSupported;
     } else {
         // 2 policy waves (3 waves per workgroup: each its own SIMD, the sim
-        // wave with the SIMD's whole register file, no scratch).  4 (5 waves:
-        // two share a SIMD, the 256-register budget, 45 spilled VGPRs and a
-        // scratch launch) measured ahead at 8 192 worlds in round 5 (9.66 ->
+        // wave with the SIMD's whole register file, no spill).  4 (5 waves:
+        // two share a SIMD, the 256-register budget, 45 spilled VGPRs)
+        // measured ahead at 8 192 worlds in round 5 (9.66 ->
         // 9.48 us per step, profiles/r05/ad_pw_ab.txt) and behind in round 6
         // (9.80 vs 9.62, three interleaved pairs, profiles/r06/o_ppo_pw_ab.txt;
         // per call 22.3 + 8.99 us per step vs 18.9 + 8.84); 16 384: 18.2 vs 12.1.

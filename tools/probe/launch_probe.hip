@@ -13,8 +13,10 @@ __global__ __launch_bounds__(320, 1) void k_probe(float *out, int iters, int idx
     __shared__ float lds[11 * 1024];
     float acc = threadIdx.x;
     if constexpr (SCRATCH) {
+        // the private array is touched only when iters > 0: at iters = 0 the
+        // launch carries a scratch allocation and no scratch traffic
         volatile float priv[40];
-        for (int i = 0; i < 40; i++) priv[i] = acc + i;
+        for (int i = 0; i < iters && i < 40; i++) priv[i] = acc + i;
         for (int i = 0; i < iters; i++) acc = acc * 0.999f + priv[(i + idx) % 40];
     } else {
         for (int i = 0; i < iters; i++) acc = acc * 0.999f + (float)((i + idx) % 40);
