@@ -1276,12 +1276,16 @@ __device__ __forceinline__ void ppo_policy_wave(const Params &p, const PolicyRol
             a.act_out = r.act_out ? r.act_out + (int64_t)t * W * 6 : nullptr;
             a.log_prob = r.log_prob ? r.log_prob + (int64_t)t * W : nullptr;
             a.value = r.value ? r.value + (int64_t)t * W : nullptr;
+            // the actions first (all the sim wave waits for), the log-probs
+            // and the records behind the hand-off
+            BucketHold<RW> hold;
             if (r.stochastic)
-                bucket_pass_spread<RW, true>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise);
+                bucket_pass_act<RW, true>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, &noise, hold);
             else
-                bucket_pass_spread<RW, false>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr);
+                bucket_pass_act<RW, false>(a, lt + rh, row0 + rh, lane, L.bucket[pw], L.act + r0 + rh, nullptr, hold);
             pol_wave_sync();
             lds_barrier();  // actions in LDS
+            bucket_pass_out<RW>(a, lt + rh, row0 + rh, lane, L.bucket[pw], hold);
             // while the sim wave steps: buffer.obs[t] = X (this wave's rows),
             // then the next step's sampling uniforms
             if (r.obs_out) {

@@ -325,6 +325,141 @@ __device__ __forceinline__ void bucket_pass_spread(const PolicyArgs &a, float (*
     }
 }
 
+// bucket_pass_spread in two halves, for a caller whose consumer needs the
+// actions before the log-probabilities (the fused PPO rollout: the sim wave
+// waits for the actions only).  bucket_pass_act runs every bucket's logits,
+// maximum, exp terms, sum and action and puts the row's six actions into
+// act_local; what the log-probability needs (maximum, sum, the chosen logit)
+// stays in the lane's registers (BucketHold).  bucket_pass_out then computes
+// logit - (max + log(sum)) per bucket and the outputs -- the same operations
+// on the same values as bucket_pass_spread, so rows are bit-identical; only
+// the order of the two halves around the caller's hand-off differs.
+template <int R>
+struct BucketHold {
+    static constexpr int BPL = (POL_BUCKETS + 64 / R - 1) / (64 / R);
+    float mx[BPL], sum[BPL], la[BPL];
+};
+
+template <int R, bool PRE = false>
+__device__ __forceinline__ void bucket_pass_act(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
+                                                BucketLds<R> &buf, int32_t (*act_local)[6], const BucketNoise<R> *pre,
+                                                BucketHold<R> &hold)
+{
+    static_assert(R == 8 || R == 16 || R == 32, "rows per bucket pass");
+    constexpr int LPR = 64 / R;
+    constexpr int BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    int32_t (*abuf)[POL_BUCKETS] = buf.a;
+    const int r = lane / LPR, part = lane % LPR;
+    const int64_t rr = row0 + r;
+    const bool live = rr < a.rows;
+    const bool stochastic = a.stochastic != 0;
+    const float *lg = tile[r];
+    BucketNoise<R> own;
+    if constexpr (!PRE) {
+        if (stochastic) bucket_noise<R>(own, a.seed, a.step, row0, a.rows, lane, a.key_row0);
+    }
+    const auto round = [&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        if constexpr (j < BPL) {
+            constexpr int NBM = bucket_round_max(LPR, j);
+            const int b = part + LPR * j;
+            hold.mx[j] = 0.f; hold.sum[j] = 1.f; hold.la[j] = 0.f;
+            if (b < POL_BUCKETS) {
+                const int o = pol_bucket_off(b), nb = pol_bucket(b);
+                float l[NBM];
+#pragma unroll
+                for (int i = 0; i < NBM; i++) {
+                    const float li = lg[o + i];
+                    l[i] = i < nb ? li : 0.f;
+                }
+                float mx = l[0];
+#pragma unroll
+                for (int i = 1; i < NBM; i++)
+                    if (i < nb) mx = l[i] > mx ? l[i] : mx;
+                float e[NBM];
+#pragma unroll
+                for (int i = 0; i < NBM; i++) e[i] = pol_expf(l[i] - mx);
+                float sum = e[0];
+#pragma unroll
+                for (int i = 1; i < NBM; i++)
+                    if (i < nb) sum = sum + e[i];
+                int act = 0;
+                if (stochastic) {
+                    const float u = PRE ? pre->u[j] : own.u[j];
+                    const float t = u * sum;
+                    float cs = 0.f;
+                    act = nb - 1;
+#pragma unroll
+                    for (int i = 0; i < NBM - 1; i++) {
+                        const bool in = i < nb - 1;
+                        const float ci = cs + e[i];
+                        act = (in && act == nb - 1 && ci > t) ? i : act;
+                        cs = in ? ci : cs;
+                    }
+                } else {
+                    float best = l[0];
+#pragma unroll
+                    for (int i = 1; i < NBM; i++) {
+                        const bool up = i < nb && l[i] > best;
+                        best = up ? l[i] : best;
+                        act = up ? i : act;
+                    }
+                }
+                float la = l[0];
+#pragma unroll
+                for (int i = 1; i < NBM; i++) la = act == i ? l[i] : la;
+                abuf[r][b] = act;
+                hold.mx[j] = mx; hold.sum[j] = sum; hold.la[j] = la;
+            }
+        }
+    };
+    round(std::integral_constant<int, 0>());
+    round(std::integral_constant<int, 1>());
+    round(std::integral_constant<int, 2>());
+    pol_wave_sync();
+    if (part == 0 && live) {
+#pragma unroll
+        for (int b = 0; b < 6; b++) act_local[r][b] = abuf[r][b];
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void bucket_pass_out(const PolicyArgs &a, float (*tile)[33], int64_t row0, int lane,
+                                                BucketLds<R> &buf, const BucketHold<R> &hold)
+{
+    constexpr int LPR = 64 / R;
+    constexpr int BPL = (POL_BUCKETS + LPR - 1) / LPR;
+    float (*tbuf)[POL_BUCKETS] = buf.t;
+    int32_t (*abuf)[POL_BUCKETS] = buf.a;
+    const int r = lane / LPR, part = lane % LPR;
+    const int64_t rr = row0 + r;
+    const bool live = rr < a.rows;
+#pragma unroll
+    for (int j = 0; j < BPL; j++) {
+        const int b = part + LPR * j;
+        if (b < POL_BUCKETS) {
+            const float lse = hold.mx[j] + pol_logf(hold.sum[j]);
+            tbuf[r][b] = hold.la[j] - lse;
+        }
+    }
+    pol_wave_sync();
+    if (part == 0 && live) {
+        float term[POL_BUCKETS];
+        int32_t act[POL_BUCKETS];
+#pragma unroll
+        for (int b = 0; b < POL_BUCKETS; b++) { term[b] = tbuf[r][b]; act[b] = abuf[r][b]; }
+        const float lp = pol_logp_sum(term);
+        if (a.act_out) {
+            int2 *d = (int2 *)(a.act_out + rr * 6);
+            d[0] = make_int2(act[0], act[1]);
+            d[1] = make_int2(act[2], act[3]);
+            d[2] = make_int2(act[4], act[5]);
+        }
+        if (a.log_prob) a.log_prob[rr] = lp;
+        if (a.value) a.value[rr] = tile[r][POL_LOGITS];
+    }
+}
+
 // The network's weights in LDS, shared by the waves of a workgroup (k_policy_wg,
 // k_step_ppo): images conflict-free for the lanes' 16-byte reads (lane (c, q)
 // reads W[16t + c][k-chunk q]): planes [q][n][j] padded to 36 / 12 floats
