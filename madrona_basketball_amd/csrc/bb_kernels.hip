@@ -1191,13 +1191,14 @@ __device__ __forceinline__ void ppo_sim_wave(const Params &p, const PolicyRollou
         wave_sync();
         lds_barrier();  // pass 0 of X: the policy waves start layer 1
         ppo_x_pass<1>(v, c, sh, active, is_trainee, split, fast, xr, ib);
+        wave_sync();
+        lds_barrier();  // X holds the observations after step t
         if (t + 1 == r.steps) {  // the sim's observation tensor: every row of the last step
+            // (beside the policy waves' value pass, which reads X only)
             obs_pass_wave<N, 0>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
             wave_sync();
             obs_pass_wave<N, 1>(v, c, ib, share, k, lane_t, w0, w_t, active, tile, p.c.obs);
         }
-        wave_sync();
-        lds_barrier();  // X holds the observations after step t
         // reward (read by nothing on the way to the next actions) while the
         // policy waves run the network on X
         if (active) {

@@ -11,7 +11,7 @@ for i in $(seq "$PAIRS"); do
     for v in base "$V"; do
         if [ "$v" = base ]; then lib=""; else lib=$LIB; fi
         echo "=== pair $i $v"
-        MADRONA_BB_LIB=$lib timeout -k 10 240 python3 "$R/tools/ppo_k_sweep.py" --worlds "$W" --ks 8,32,64 --calls 30 \
+        MADRONA_BB_LIB=$lib timeout -k 10 240 python3 "$R/tools/ppo_k_sweep.py" --worlds "$W" --ks "${KS:-8,32,64}" --calls 30 \
             > "$OUT/tmp.log" 2>&1 || { cat "$OUT/tmp.log"; exit 1; }
         grep -v amdgpu.ids "$OUT/tmp.log" | sed "s/^/$v: /" | tee -a "$OUT/ab.txt"
     done
