@@ -198,7 +198,8 @@ def main():
                          "(WORLD_SIZE); they must agree")
     rank = int(os.environ.get("RANK", "0"))
     cpu = cpu_exec = None
-    if rank == 0 and not args.no_cpu_baseline:  # before any GPU call (the other ranks wait at init)
+    # the CPU baselines: rank 0 at N = 1 only, before any GPU call
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.agents, args.cpu_seconds, args.cpu_procs)
         cpu_exec = cpu_executor_baseline(args.agents, min(args.cpu_seconds, 8.0), args.cpu_procs)
 
